@@ -1,0 +1,77 @@
+"""ctypes binding of ``libcram_attn.so`` (the C-ABI of ``include/cram_attn.h``).
+
+There is no fallback: if the HIP library is missing the product path raises.
+torch is imported first so that the HIP runtime torch ships
+(``libamdhip64.so.7``) is the one the library binds to.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_float, c_int, c_int64, c_size_t, c_void_p, POINTER
+
+import torch  # noqa: F401  (loads the HIP runtime before the library)
+
+from .build import LIB_PATH
+
+_c_int32_p = POINTER(ctypes.c_int32)
+_c_uint8_p = POINTER(ctypes.c_uint8)
+_c_float_p = POINTER(c_float)
+
+# name -> (restype, argtypes); the exact export list of include/cram_attn.h
+SIGNATURES = {
+    "cram_strerror": (ctypes.c_char_p, [c_int]),
+    "cram_abi_version": (c_int, []),
+    "cram_attn_prefill": (c_int, [
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+        c_void_p, c_int64, c_void_p, c_int64, c_int,
+        c_void_p,
+    ]),
+    "cram_attn_decode_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "cram_attn_decode": (c_int, [
+        c_void_p, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64,
+        c_int, c_int, c_int, c_int, c_void_p, c_int, c_float,
+        c_void_p, c_int64, c_void_p, c_int64, c_int,
+        c_int, c_void_p, c_size_t,
+        c_void_p,
+    ]),
+    "cram_answer_logits": (c_int, [
+        c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+    ]),
+}
+
+_LIB = None
+
+
+class CrAMLibraryError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise CrAMLibraryError(
+            f"{LIB_PATH} is missing: build it with `python -m cram_amd.build` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = ctypes.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(code: int, what: str) -> None:
+    if code != 0:
+        msg = load().cram_strerror(code).decode()
+        raise RuntimeError(f"{what} failed: CRAM error {code} ({msg})")

@@ -1,0 +1,621 @@
+// cram_attn.hip — credibility-biased causal GQA attention for MI355X (gfx950, CDNA4).
+//
+// Replaces the reference's dense-mask forward-pre-hook
+// (/root/reference/utils/re_weighting.py:36-61, registered at :118-124 and :163-168)
+// plus the SDPA call it feeds.  The hook writes bf16(log_fp16(w_j)) into every
+// causal-allowed mask entry of the selected heads; here the same value arrives as
+// a per-key fp32 bias vector and is added to the fp32 scores inside the kernel.
+//
+// Kernels
+//   prefill_kernel<D>        flash attention, bf16 MFMA v_mfma_f32_32x32x16_bf16,
+//                            "swapped" S^T = K.Q^T so each lane owns one query row
+//                            (row softmax is lane-local + one permlane32 swap),
+//                            O^T += V^T.P^T with P taken straight from the S^T
+//                            accumulator registers and V^T read with
+//                            ds_read_b64_tr_b16 from a row-major LDS image.
+//                            K/V/bias tiles register-staged into double-buffered
+//                            LDS (issue early, write late, one barrier per tile).
+//   decode_kernel<D,G>       q_len == 1, HBM-bound: 16 lanes per key row (16 B each),
+//                            all G query heads of a kv head per workgroup, optional
+//                            split over keys + combine_kernel.
+//   answer_logits_kernel     fp32 dot of hidden rows with gathered lm_head rows.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/cram_attn.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kNegInf = -__builtin_huge_valf();
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// value from lane l^32 combined with own value (lane halves exchanged by one permlane32 swap)
+__device__ __forceinline__ float half_max(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// --------------------------------------------------------------------------------------------
+// prefill
+// --------------------------------------------------------------------------------------------
+struct PrefillParams {
+  const __bf16* q; int64_t q_sb, q_sh, q_st;
+  const __bf16* k; int64_t k_sb, k_sh, k_st;
+  const __bf16* v; int64_t v_sb, v_sh, v_st;
+  __bf16* o; int64_t o_sb, o_sh, o_st;
+  const float* bias; int64_t bias_sb;
+  const uint8_t* enable; int64_t en_sb;
+  int B, Hq, Hkv, Tq, S, W, q_pos0;
+  float scale_log2;  // softmax scale * log2(e)
+  int nqb, nblocks;
+};
+
+template <int D>
+struct PrefillCfg {
+  static constexpr int BQ = 128;              // query rows per workgroup (4 waves x 32)
+  static constexpr int BK = 64;               // keys per tile
+  static constexpr int KSTR = D * 2 + 16;     // K image row stride (bytes): conflict-free ds_read_b128
+  static constexpr int VSTR = D * 2 + 64;     // V image row stride (bytes): conflict-free ds_read_b64_tr_b16
+  static constexpr int K_BYTES = BK * KSTR;
+  static constexpr int V_BYTES = BK * VSTR;
+  static constexpr int B_BYTES = BK * 4;
+  static constexpr int STAGE = K_BYTES + V_BYTES + B_BYTES;
+  static constexpr int LDS = 2 * STAGE;
+  static constexpr int CPR = D / 8;           // 16-byte chunks per row
+  static constexpr int CPT = BK * CPR / 256;  // chunks per thread per tile
+};
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
+  using C = PrefillCfg<D>;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+
+  // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each XCD a
+  // contiguous run of work ids (all query blocks of a head -> one L2 for its K/V).
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int qi_blk = wid % p.nqb;
+  const int bh = wid / p.nqb;
+  const int hq = bh % p.Hq;
+  const int b = bh / p.Hq;
+  const int qblk = p.nqb - 1 - qi_blk;  // heaviest (longest causal range) first
+  const int G = p.Hq / p.Hkv;
+  const int hkv = hq / G;
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q_row0 = qblk * C::BQ + wave * 32;
+  const int qrow = q_row0 + r;
+  const int qpos = p.q_pos0 + qrow;
+
+  const __bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const __bf16* kbase = p.k + b * p.k_sb + hkv * p.k_sh;
+  const __bf16* vbase = p.v + b * p.v_sb + hkv * p.v_sh;
+  const bool en = (p.bias != nullptr) && (p.enable != nullptr) && p.enable[b * p.en_sb + hq] != 0;
+  const float* brow = en ? p.bias + b * p.bias_sb : nullptr;
+
+  // Q as the B operand of S^T = K.Q^T: lane (r, hh) holds Q[qrow][16ks + 8hh .. +7]
+  bf16x8 qf[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    if (qrow < p.Tq) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qb + qrow * p.q_st + 16 * ks + 8 * hh);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)0.f;
+    }
+  }
+
+  const int blk_last_q = min(qblk * C::BQ + C::BQ, p.Tq) - 1;
+  const int kv_end = min(p.S, p.q_pos0 + blk_last_q + 1);
+  const int nt = (kv_end + C::BK - 1) / C::BK;
+  const bool wave_live = q_row0 < p.Tq;
+  const int wave_qpos_min = p.q_pos0 + q_row0;
+  const int wave_qpos_max = p.q_pos0 + min(q_row0 + 31, p.Tq - 1);
+
+  uint4 kst[C::CPT], vst[C::CPT];
+  float bst = 0.f;
+
+  auto gload = [&](int t) {
+    const int key0 = t * C::BK;
+#pragma unroll
+    for (int i = 0; i < C::CPT; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c / C::CPR, col = c % C::CPR;
+      const int key = key0 + row;
+      if (key < p.S) {
+        kst[i] = *reinterpret_cast<const uint4*>(kbase + key * p.k_st + col * 8);
+        vst[i] = *reinterpret_cast<const uint4*>(vbase + key * p.v_st + col * 8);
+      } else {
+        kst[i] = make_uint4(0, 0, 0, 0);
+        vst[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    if (tid < C::BK) {
+      const int key = key0 + tid;
+      bst = (en && key < p.W) ? brow[key] * kLog2e : 0.f;
+    }
+  };
+  auto swrite = [&](int buf) {
+    char* base = smem + buf * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::CPT; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c / C::CPR, col = c % C::CPR;
+      *reinterpret_cast<uint4*>(base + row * C::KSTR + col * 16) = kst[i];
+      *reinterpret_cast<uint4*>(base + C::K_BYTES + row * C::VSTR + col * 16) = vst[i];
+    }
+    if (tid < C::BK) reinterpret_cast<float*>(base + C::K_BYTES + C::V_BYTES)[tid] = bst;
+  };
+
+  float m = kNegInf, l = 0.f;
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) oacc[db][e] = 0.f;
+
+  // per-lane constant LDS offsets
+  const int g16 = lane >> 4, i16 = lane & 15;
+  const int tr_key = 4 * (g16 >> 1) + (i16 >> 2);              // + kb*32 + 16s (+8)
+  const int tr_col = 16 * (g16 & 1) + 4 * (i16 & 3);            // + db*32
+
+  if (nt > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) gload(t + 1);
+    const int key0 = t * C::BK;
+    if (wave_live && key0 <= wave_qpos_max) {
+      const char* base = smem + (t & 1) * C::STAGE;
+      f32x16 sacc[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sacc[kb][e] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
+          sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
+        }
+      }
+      // scores (log2 units): scale, credibility bias, causal / length mask
+      const float* bl = reinterpret_cast<const float*>(base + C::K_BYTES + C::V_BYTES);
+      const bool need_mask = (key0 + C::BK - 1 > wave_qpos_min) || (key0 + C::BK > p.S);
+      const int lim = min(qpos, p.S - 1) - key0;
+      float mx = kNegInf;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+          if (en) bv = *reinterpret_cast<const f32x4*>(bl + kb * 32 + 8 * g + 4 * hh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float s = sacc[kb][4 * g + e] * p.scale_log2 + bv[e];
+            // branch-free causal / length mask: key offset in tile vs the lane's last allowed key
+            s = (need_mask && (kb * 32 + 8 * g + 4 * hh + e > lim)) ? kNegInf : s;
+            sacc[kb][4 * g + e] = s;
+            mx = fmaxf(mx, s);
+          }
+        }
+      }
+      mx = half_max(mx);
+      const float mnew = fmaxf(m, mx);
+      const float muse = (mnew == kNegInf) ? 0.f : mnew;
+      const float alpha = fast_exp2(m - muse);
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float pe = fast_exp2(sacc[kb][e] - muse);
+          sacc[kb][e] = pe;
+          rs += pe;
+        }
+      rs = half_sum(rs);
+      l = l * alpha + rs;
+      m = mnew;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) oacc[db][e] *= alpha;
+
+      // O^T[dv][q] += V^T[dv][key] . P^T[key][q]
+      const char* vimg = base + C::K_BYTES;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 pb;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sacc[kb][8 * s + j];
+          const int key_a = kb * 32 + 16 * s + tr_key;
+#pragma unroll
+          for (int db = 0; db < D / 32; ++db) {
+            const int col = db * 32 + tr_col;
+            const i16x4 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(vimg + key_a * C::VSTR + col * 2));
+            const i16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_i16x4*)(vimg + (key_a + 8) * C::VSTR + col * 2));
+            // whole-vector bit cast (per-element extraction of the tr result miscompiles on ROCm 7.2)
+            const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pb, oacc[db], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (t + 1 < nt) swrite((t + 1) & 1);
+    __syncthreads();
+  }
+
+  if (qrow < p.Tq) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    __bf16* ob = p.o + b * p.o_sb + hq * p.o_sh + qrow * p.o_st;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 o4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o4[e] = (__bf16)(oacc[db][4 * g + e] * inv);
+        *reinterpret_cast<bf16x4*>(ob + db * 32 + 8 * g + 4 * hh) = o4;
+      }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// decode (q_len == 1)
+// --------------------------------------------------------------------------------------------
+struct DecodeParams {
+  const __bf16* q; int64_t q_sb, q_sh;
+  const __bf16* k; int64_t k_sb, k_sh, k_st;
+  const __bf16* v; int64_t v_sb, v_sh, v_st;
+  __bf16* o; int64_t o_sb, o_sh;
+  const float* bias; int64_t bias_sb;
+  const uint8_t* enable; int64_t en_sb;
+  const int32_t* seq_lens;
+  int B, Hq, Hkv, S, W;
+  float scale_log2;
+  float* ws_o;   // [B][Hq][nsplit][D] unnormalised partial outputs (split mode)
+  float* ws_ml;  // [B][Hq][nsplit][2]  partial (max, sum)
+};
+
+template <int D, int G>
+__global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
+  constexpr int LPK = D / 8;        // lanes per key row (8 bf16 = 16 B per lane)
+  constexpr int KPW = 64 / LPK;     // keys per wave-instruction
+  constexpr int U = 4;              // keys per lane group per iteration
+  constexpr int STEP = 4 * KPW;     // keys per workgroup per unrolled slot
+  __shared__ float red_m[4][G], red_l[4][G];
+  __shared__ float red_o[4][G][D];
+
+  const int hkv = blockIdx.x, b = blockIdx.y, split = blockIdx.z, nsplit = gridDim.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int grp = lane / LPK, li = lane % LPK;
+
+  const int S_b = p.seq_lens ? p.seq_lens[b] : p.S;
+  const int chunk = (((S_b + nsplit - 1) / nsplit) + 63) & ~63;
+  const int k_begin = split * chunk;
+  const int k_end = min(S_b, k_begin + chunk);
+
+  float qv[G][8];
+  bool en[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int hq = hkv * G + g;
+    const bf16x8 qq = *reinterpret_cast<const bf16x8*>(p.q + b * p.q_sb + hq * p.q_sh + li * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qv[g][j] = (float)qq[j] * p.scale_log2;
+    en[g] = (p.bias != nullptr) && (p.enable != nullptr) && p.enable[b * p.en_sb + hq] != 0;
+  }
+  const float* brow = p.bias ? p.bias + b * p.bias_sb : nullptr;
+  const __bf16* kbase = p.k + b * p.k_sb + hkv * p.k_sh + li * 8;
+  const __bf16* vbase = p.v + b * p.v_sb + hkv * p.v_sh + li * 8;
+
+  float m[G], l[G], acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    m[g] = kNegInf;
+    l[g] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
+  }
+
+  for (int key_base = k_begin + wave * KPW + grp; key_base < k_end; key_base += U * STEP) {
+    bf16x8 kr[U], vr[U];
+    bool valid[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int key = key_base + u * STEP;
+      valid[u] = key < k_end;
+      if (valid[u]) {
+        kr[u] = *reinterpret_cast<const bf16x8*>(kbase + key * p.k_st);
+        vr[u] = *reinterpret_cast<const bf16x8*>(vbase + key * p.v_st);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kr[u][j] = (__bf16)0.f; vr[u][j] = (__bf16)0.f; }
+      }
+    }
+    float bias_u[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int key = key_base + u * STEP;
+      bias_u[u] = (brow && valid[u] && key < p.W) ? brow[key] * kLog2e : 0.f;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float s[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += qv[g][j] * (float)kr[u][j];
+#pragma unroll
+        for (int off = LPK / 2; off >= 1; off >>= 1) d += __shfl_xor(d, off, 64);
+        s[u] = valid[u] ? d + (en[g] ? bias_u[u] : 0.f) : kNegInf;
+      }
+      float mx = s[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u) mx = fmaxf(mx, s[u]);
+      const float mnew = fmaxf(m[g], mx);
+      const float muse = (mnew == kNegInf) ? 0.f : mnew;
+      const float alpha = fast_exp2(m[g] - muse);
+      l[g] *= alpha;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[g][j] *= alpha;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float pu = fast_exp2(s[u] - muse);
+        l[g] += pu;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[g][j] += pu * (float)vr[u][j];
+      }
+      m[g] = mnew;
+    }
+  }
+
+  // combine the lane groups of this wave (groups differ by lane bits above log2(LPK))
+#pragma unroll
+  for (int off = LPK; off < 64; off <<= 1) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float mo = __shfl_xor(m[g], off, 64);
+      const float lo = __shfl_xor(l[g], off, 64);
+      const float mnew = fmaxf(m[g], mo);
+      const float muse = (mnew == kNegInf) ? 0.f : mnew;
+      const float a0 = fast_exp2(m[g] - muse), a1 = fast_exp2(mo - muse);
+      l[g] = l[g] * a0 + lo * a1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float ao = __shfl_xor(acc[g][j], off, 64);
+        acc[g][j] = acc[g][j] * a0 + ao * a1;
+      }
+      m[g] = mnew;
+    }
+  }
+  if (grp == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (li == 0) { red_m[wave][g] = m[g]; red_l[wave][g] = l[g]; }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red_o[wave][g][li * 8 + j] = acc[g][j];
+    }
+  }
+  __syncthreads();
+  // combine the 4 waves: thread t handles (g, dim) pairs
+  for (int idx = tid; idx < G * D; idx += 256) {
+    const int g = idx / D, dd = idx % D;
+    float M = kNegInf;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, red_m[w][g]);
+    const float Muse = (M == kNegInf) ? 0.f : M;
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float a = fast_exp2(red_m[w][g] - Muse);
+      L += red_l[w][g] * a;
+      O += red_o[w][g][dd] * a;
+    }
+    const int hq = hkv * G + g;
+    if (nsplit == 1) {
+      p.o[b * p.o_sb + hq * p.o_sh + dd] = (__bf16)(L > 0.f ? O / L : 0.f);
+    } else {
+      const int64_t slot = ((int64_t)(b * p.Hq + hq) * nsplit + split);
+      p.ws_o[slot * D + dd] = O;
+      if (dd == 0) { p.ws_ml[slot * 2 + 0] = M; p.ws_ml[slot * 2 + 1] = L; }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void decode_combine_kernel(DecodeParams p, int nsplit) {
+  const int hq = blockIdx.x, b = blockIdx.y, dd = threadIdx.x;
+  const int64_t slot0 = (int64_t)(b * p.Hq + hq) * nsplit;
+  float M = kNegInf;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, p.ws_ml[(slot0 + s) * 2]);
+  const float Muse = (M == kNegInf) ? 0.f : M;
+  float L = 0.f, O = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float a = fast_exp2(p.ws_ml[(slot0 + s) * 2] - Muse);
+    L += p.ws_ml[(slot0 + s) * 2 + 1] * a;
+    O += p.ws_o[(slot0 + s) * D + dd] * a;
+  }
+  p.o[b * p.o_sb + hq * p.o_sh + dd] = (__bf16)(L > 0.f ? O / L : 0.f);
+}
+
+// --------------------------------------------------------------------------------------------
+// answer-token logits
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void answer_logits_kernel(const __bf16* h, int64_t h_rs, const __bf16* w,
+                                                            int64_t w_rs, const int32_t* ids, int n, int D,
+                                                            int round_bf16, float* out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const __bf16* hr = h + row * h_rs;
+  const __bf16* wr = w + (int64_t)ids[row] * w_rs;
+  float acc = 0.f;
+  for (int d0 = lane * 8; d0 < D; d0 += 512) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(hr + d0);
+    const bf16x8 c = *reinterpret_cast<const bf16x8*>(wr + d0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += (float)a[j] * (float)c[j];
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) out[row] = round_bf16 ? (float)(__bf16)acc : acc;
+}
+
+// --------------------------------------------------------------------------------------------
+// host helpers
+// --------------------------------------------------------------------------------------------
+inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+inline bool m8(int64_t s) { return (s & 7) == 0; }
+
+template <int D>
+int launch_prefill(PrefillParams& p, hipStream_t stream) {
+  using C = PrefillCfg<D>;
+  p.nqb = (p.Tq + C::BQ - 1) / C::BQ;
+  const int64_t nblocks = (int64_t)p.nqb * p.Hq * p.B;
+  if (nblocks > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
+  p.nblocks = (int)nblocks;
+  hipLaunchKernelGGL(prefill_kernel<D>, dim3(p.nblocks), dim3(256), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}
+
+template <int D, int G>
+int launch_decode_g(DecodeParams& p, int nsplit, hipStream_t stream) {
+  hipLaunchKernelGGL((decode_kernel<D, G>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+  if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
+  if (nsplit > 1) {
+    hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(p.Hq, p.B), dim3(D), 0, stream, p, nsplit);
+    if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
+  }
+  return CRAM_OK;
+}
+
+template <int D>
+int launch_decode(DecodeParams& p, int G, int nsplit, hipStream_t stream) {
+  switch (G) {
+    case 1: return launch_decode_g<D, 1>(p, nsplit, stream);
+    case 2: return launch_decode_g<D, 2>(p, nsplit, stream);
+    case 4: return launch_decode_g<D, 4>(p, nsplit, stream);
+    case 7: return launch_decode_g<D, 7>(p, nsplit, stream);
+    case 8: return launch_decode_g<D, 8>(p, nsplit, stream);
+    default: return CRAM_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cram_strerror(int code) {
+  switch (code) {
+    case CRAM_OK: return "ok";
+    case CRAM_ERR_INVALID_ARG: return "invalid argument";
+    case CRAM_ERR_UNSUPPORTED: return "unsupported head dim or GQA group size";
+    case CRAM_ERR_ALIGNMENT: return "stride not a multiple of 8 elements or pointer not 16-byte aligned";
+    case CRAM_ERR_LAUNCH: return "kernel launch failed";
+    case CRAM_ERR_WORKSPACE: return "split-S workspace missing or too small";
+    default: return "unknown error";
+  }
+}
+
+int cram_abi_version(void) { return 1; }
+
+int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sb,
+                      int64_t k_sh, int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st, void* o,
+                      int64_t o_sb, int64_t o_sh, int64_t o_st, int B, int Hq, int Hkv, int Tq, int S, int d,
+                      int q_pos0, float scale, const float* bias, int64_t bias_sb, const uint8_t* enable,
+                      int64_t en_sb, int W, cram_stream_t stream) {
+  if (!q || !k || !v || !o) return CRAM_ERR_INVALID_ARG;
+  if (B <= 0 || Hq <= 0 || Hkv <= 0 || Tq <= 0 || S <= 0 || Hq % Hkv != 0 || q_pos0 < 0) return CRAM_ERR_INVALID_ARG;
+  if (d != 64 && d != 128) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return CRAM_ERR_ALIGNMENT;
+  if (!m8(q_sb) || !m8(q_sh) || !m8(q_st) || !m8(k_sb) || !m8(k_sh) || !m8(k_st) || !m8(v_sb) || !m8(v_sh) ||
+      !m8(v_st) || !m8(o_sb) || !m8(o_sh) || !m8(o_st))
+    return CRAM_ERR_ALIGNMENT;
+  if (bias && W < 0) return CRAM_ERR_INVALID_ARG;
+  PrefillParams p;
+  p.q = (const __bf16*)q; p.q_sb = q_sb; p.q_sh = q_sh; p.q_st = q_st;
+  p.k = (const __bf16*)k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = (const __bf16*)v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = (__bf16*)o; p.o_sb = o_sb; p.o_sh = o_sh; p.o_st = o_st;
+  p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
+  p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
+  p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = Tq; p.S = S; p.W = bias ? W : 0; p.q_pos0 = q_pos0;
+  p.scale_log2 = scale * kLog2e;
+  return d == 128 ? launch_prefill<128>(p, (hipStream_t)stream) : launch_prefill<64>(p, (hipStream_t)stream);
+}
+
+size_t cram_attn_decode_workspace_size(int B, int Hq, int d, int num_splits) {
+  if (num_splits <= 1 || B <= 0 || Hq <= 0 || d <= 0) return 0;
+  return (size_t)B * Hq * num_splits * (size_t)(d + 2) * sizeof(float);
+}
+
+int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh, const void* k, int64_t k_sb, int64_t k_sh,
+                     int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st, void* o, int64_t o_sb,
+                     int64_t o_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d, float scale,
+                     const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                     int num_splits, void* workspace, size_t workspace_bytes, cram_stream_t stream) {
+  if (!q || !k || !v || !o) return CRAM_ERR_INVALID_ARG;
+  if (B <= 0 || Hq <= 0 || Hkv <= 0 || S <= 0 || Hq % Hkv != 0 || num_splits <= 0 || B > 65535 ||
+      num_splits > 65535)
+    return CRAM_ERR_INVALID_ARG;
+  if (d != 64 && d != 128) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(q) || !al16(k) || !al16(v)) return CRAM_ERR_ALIGNMENT;
+  if (!m8(q_sb) || !m8(q_sh) || !m8(k_sb) || !m8(k_sh) || !m8(k_st) || !m8(v_sb) || !m8(v_sh) || !m8(v_st))
+    return CRAM_ERR_ALIGNMENT;
+  if (bias && W < 0) return CRAM_ERR_INVALID_ARG;
+  DecodeParams p;
+  p.q = (const __bf16*)q; p.q_sb = q_sb; p.q_sh = q_sh;
+  p.k = (const __bf16*)k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = (const __bf16*)v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = (__bf16*)o; p.o_sb = o_sb; p.o_sh = o_sh;
+  p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
+  p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
+  p.seq_lens = seq_lens;
+  p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.S = S; p.W = bias ? W : 0;
+  p.scale_log2 = scale * kLog2e;
+  p.ws_o = nullptr; p.ws_ml = nullptr;
+  if (num_splits > 1) {
+    const size_t need = cram_attn_decode_workspace_size(B, Hq, d, num_splits);
+    if (!workspace || workspace_bytes < need || !al16(workspace)) return CRAM_ERR_WORKSPACE;
+    p.ws_o = (float*)workspace;
+    p.ws_ml = p.ws_o + (size_t)B * Hq * num_splits * d;
+  }
+  const int G = Hq / Hkv;
+  return d == 128 ? launch_decode<128>(p, G, num_splits, (hipStream_t)stream)
+                  : launch_decode<64>(p, G, num_splits, (hipStream_t)stream);
+}
+
+int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64_t w_rs, const int32_t* ids, int n,
+                       int D, int round_bf16, float* out, cram_stream_t stream) {
+  if (!hidden || !w_lm || !ids || !out || n < 0 || D <= 0) return CRAM_ERR_INVALID_ARG;
+  if (n == 0) return CRAM_OK;
+  if ((D & 7) || !m8(h_rs) || !m8(w_rs) || !al16(hidden) || !al16(w_lm)) return CRAM_ERR_ALIGNMENT;
+  hipLaunchKernelGGL(answer_logits_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)hidden, h_rs, (const __bf16*)w_lm, w_rs, ids, n, D, round_bf16, out);
+  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+"""torch-tensor front end of the C-ABI (device memory + stream plumbing only).
+
+Every function here validates shapes/dtypes on the host, then enqueues the HIP
+kernel on torch's current stream through ``include/cram_attn.h``.  Nothing
+falls back to PyTorch math: a missing library or a rejected shape raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check_bf16(name: str, t: torch.Tensor, ndim: int) -> None:
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name} must be bfloat16, got {t.dtype}")
+    if t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name} must have a contiguous last dimension")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+
+
+def _bias_args(bias, enable, B, Hq, W):
+    if bias is None or enable is None:
+        return None, 0, None, 0, 0
+    if bias.dtype != torch.float32 or bias.dim() != 2 or bias.shape[0] != B or bias.stride(1) != 1:
+        raise ValueError("bias must be float32 [B, S] with a contiguous last dim")
+    if enable.dtype != torch.uint8 or enable.dim() != 2 or enable.shape != (B, Hq) or enable.stride(1) != 1:
+        raise ValueError("enable must be uint8 [B, Hq]")
+    if not 0 <= W <= bias.shape[1]:
+        raise ValueError(f"W={W} outside the bias row length {bias.shape[1]}")
+    return bias.data_ptr(), bias.stride(0), enable.data_ptr(), enable.stride(0), int(W)
+
+
+def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: float, q_pos0: Optional[int] = None,
+                 bias: Optional[torch.Tensor] = None, enable: Optional[torch.Tensor] = None, W: int = 0,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Causal credibility-biased attention for q_len >= 1.
+
+    q [B, Hq, Tq, d], k/v [B, Hkv, S, d] (any strides, last dim contiguous).
+    Returns ``out`` [B, Tq, Hq, d] (the layout transformers' attention
+    interface returns); query i sits at position ``q_pos0 + i`` (default S - Tq).
+    """
+    _check_bf16("q", q, 4)
+    _check_bf16("k", k, 4)
+    _check_bf16("v", v, 4)
+    B, Hq, Tq, d = q.shape
+    _, Hkv, S, _ = k.shape
+    if k.shape[0] != B or v.shape != k.shape or k.shape[3] != d:
+        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    if q_pos0 is None:
+        q_pos0 = S - Tq
+    if out is None:
+        out = torch.empty((B, Tq, Hq, d), dtype=q.dtype, device=q.device)
+    elif out.shape != (B, Tq, Hq, d) or out.dtype != q.dtype or out.stride(-1) != 1:
+        raise ValueError("out must be bf16 [B, Tq, Hq, d] with a contiguous last dim")
+    bp, bsb, ep, esb, W = _bias_args(bias, enable, B, Hq, W)
+    lib = _lib.load()
+    code = lib.cram_attn_prefill(
+        q.data_ptr(), q.stride(0), q.stride(1), q.stride(2),
+        k.data_ptr(), k.stride(0), k.stride(1), k.stride(2),
+        v.data_ptr(), v.stride(0), v.stride(1), v.stride(2),
+        out.data_ptr(), out.stride(0), out.stride(2), out.stride(1),
+        B, Hq, Hkv, Tq, S, d, int(q_pos0), float(scale),
+        bp, bsb, ep, esb, W, _stream(q.device))
+    _lib.check(code, "cram_attn_prefill")
+    return out
+
+
+def decode_workspace_bytes(B: int, Hq: int, d: int, num_splits: int) -> int:
+    return int(_lib.load().cram_attn_decode_workspace_size(B, Hq, d, num_splits))
+
+
+def attn_decode(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: float,
+                seq_lens: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+                enable: Optional[torch.Tensor] = None, W: int = 0, num_splits: int = 1,
+                workspace: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Single-token attention.  q [B, Hq, d]; k/v [B, Hkv, S_max, d]; out [B, Hq, d].
+
+    ``seq_lens`` (int32 [B], device) gives the number of valid keys per row
+    (default: all S_max).  ``num_splits`` > 1 needs ``workspace`` (uint8, at
+    least ``decode_workspace_bytes`` bytes).
+    """
+    _check_bf16("q", q, 3)
+    _check_bf16("k", k, 4)
+    _check_bf16("v", v, 4)
+    B, Hq, d = q.shape
+    _, Hkv, S, _ = k.shape
+    if k.shape[0] != B or v.shape != k.shape or k.shape[3] != d:
+        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    if seq_lens is not None and (seq_lens.dtype != torch.int32 or seq_lens.shape != (B,) or not seq_lens.is_cuda):
+        raise ValueError("seq_lens must be a device int32 [B] tensor")
+    if out is None:
+        out = torch.empty((B, Hq, d), dtype=q.dtype, device=q.device)
+    bp, bsb, ep, esb, W = _bias_args(bias, enable, B, Hq, W)
+    lib = _lib.load()
+    ws_ptr, ws_bytes = None, 0
+    if num_splits > 1:
+        need = decode_workspace_bytes(B, Hq, d, num_splits)
+        if workspace is None:
+            workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+        ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+    code = lib.cram_attn_decode(
+        q.data_ptr(), q.stride(0), q.stride(1),
+        k.data_ptr(), k.stride(0), k.stride(1), k.stride(2),
+        v.data_ptr(), v.stride(0), v.stride(1), v.stride(2),
+        out.data_ptr(), out.stride(0), out.stride(1),
+        B, Hq, Hkv, S, _ptr(seq_lens), d, float(scale),
+        bp, bsb, ep, esb, W, int(num_splits), ws_ptr, ws_bytes, _stream(q.device))
+    _lib.check(code, "cram_attn_decode")
+    return out
+
+
+def answer_logits(hidden: torch.Tensor, w_lm: torch.Tensor, ids: torch.Tensor, *, round_bf16: bool = False,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out[i] = <hidden[i], w_lm[ids[i]]> in fp32.  hidden [n, D] bf16, w_lm [V, D] bf16, ids int32 [n]."""
+    _check_bf16("hidden", hidden, 2)
+    _check_bf16("w_lm", w_lm, 2)
+    n, D = hidden.shape
+    if w_lm.shape[1] != D or ids.dtype != torch.int32 or ids.shape != (n,):
+        raise ValueError("answer_logits: hidden [n, D], w_lm [V, D], ids int32 [n]")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=hidden.device)
+    lib = _lib.load()
+    code = lib.cram_answer_logits(hidden.data_ptr(), hidden.stride(0), w_lm.data_ptr(), w_lm.stride(0),
+                                  ids.data_ptr(), n, D, int(bool(round_bf16)), out.data_ptr(),
+                                  _stream(hidden.device))
+    _lib.check(code, "cram_answer_logits")
+    return out

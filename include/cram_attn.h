@@ -1,0 +1,106 @@
+/*
+ * cram_attn.h — C-ABI of the MI355X (gfx950) credibility-biased attention library.
+ *
+ * This is the drop-in boundary for CrAM's credibility re-weighting hot path.
+ * In the reference the path is a Python forward-pre-hook that rewrites the
+ * dense attention mask of every selected (layer, head):
+ *
+ *   /root/reference/utils/re_weighting.py:36-61   Re_Weighting_Strategy.edit_attention_mask
+ *       mask[0,h,i,j] = bf16(log_fp16(w_j))  for causal-allowed (i, j), j < W, h in head_idx
+ *   /root/reference/utils/re_weighting.py:118-124 hook registration (generate path)
+ *   /root/reference/utils/re_weighting.py:163-168 hook registration (IE sweep path)
+ *
+ * and the attention op the mask then flows into (transformers 5.15
+ * sdpa_attention_forward -> F.scaled_dot_product_attention).  Here the mask is
+ * never materialised: the kernels take an O(S) per-key bias vector plus an O(Hq)
+ * per-head enable mask and add  enable[b,h] * bias[b,j]  (for j < W) to the
+ * scaled QK^T scores inline.
+ *
+ * Conventions
+ *   - all tensor pointers are DEVICE pointers owned by the caller; no entry
+ *     point allocates, frees or synchronises;
+ *   - q/k/v/o are bf16, last dimension contiguous, every stride given in
+ *     ELEMENTS and a multiple of 8, every base pointer 16-byte aligned;
+ *   - bias is fp32 [B][bias_sb] in natural-log units (the hook's
+ *     bf16(log_fp16(w)) already widened to fp32); enable is uint8 [B][en_sb];
+ *     a NULL bias or NULL enable means "no re-weighting" (plain causal);
+ *   - work is enqueued on `stream` (a hipStream_t; NULL = default stream);
+ *   - every entry point returns CRAM_OK (0) or a negative CRAM_ERR_* code and
+ *     never aborts; cram_strerror() names the code.
+ */
+#ifndef CRAM_ATTN_H
+#define CRAM_ATTN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CRAM_OK 0
+#define CRAM_ERR_INVALID_ARG -1   /* null pointer, non-positive size, Hq % Hkv != 0 ... */
+#define CRAM_ERR_UNSUPPORTED -2   /* head dim not in {64,128}, GQA group size not supported */
+#define CRAM_ERR_ALIGNMENT -3     /* stride not a multiple of 8 elements / pointer not 16-B aligned */
+#define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
+#define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
+
+typedef void* cram_stream_t; /* hipStream_t */
+
+const char* cram_strerror(int code);
+int cram_abi_version(void);
+
+/*
+ * Prefill / multi-token attention (replaces the hooked SDPA call for
+ * q_len > 1; reference: re_weighting.py:39-59 mask build + sdpa_attention.py:154).
+ *
+ *   q : [B][Hq][Tq][d]   strides (q_sb, q_sh, q_st)
+ *   k : [B][Hkv][S][d]   strides (k_sb, k_sh, k_st)
+ *   v : [B][Hkv][S][d]   strides (v_sb, v_sh, v_st)
+ *   o : [B][Hq][Tq][d]   strides (o_sb, o_sh, o_st)   (o[b,h,i,:] may alias a [B,Tq,Hq,d] buffer)
+ *   query i sits at absolute position q_pos0 + i and attends keys j <= q_pos0 + i, j < S
+ *   score(i,j) = scale * q_i . k_j + (enable[b*en_sb+h] ? bias[b*bias_sb+j] : 0 for j < W)
+ */
+int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st,
+                      const void* k, int64_t k_sb, int64_t k_sh, int64_t k_st,
+                      const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st,
+                      void* o, int64_t o_sb, int64_t o_sh, int64_t o_st,
+                      int B, int Hq, int Hkv, int Tq, int S, int d, int q_pos0, float scale,
+                      const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                      cram_stream_t stream);
+
+/*
+ * Single-token decode attention (replaces the hooked SDPA call for q_len == 1;
+ * reference: re_weighting.py:42-44 decode mask + :57-59 bias fill).
+ *
+ *   q : [B][Hq][d] (q_sb, q_sh);  o : [B][Hq][d] (o_sb, o_sh)
+ *   k, v : [B][Hkv][S_max][d] (k_sb, k_sh, k_st) / (v_sb, v_sh, v_st)
+ *   seq_lens : device int32 [B] keys per batch row, or NULL -> every row has S keys
+ *   num_splits > 1 splits the keys of each (b, kv head) over that many workgroups;
+ *   it needs `workspace` of cram_attn_decode_workspace_size(B, Hq, d, num_splits) bytes.
+ */
+size_t cram_attn_decode_workspace_size(int B, int Hq, int d, int num_splits);
+int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh,
+                     const void* k, int64_t k_sb, int64_t k_sh, int64_t k_st,
+                     const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st,
+                     void* o, int64_t o_sb, int64_t o_sh,
+                     int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d, float scale,
+                     const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                     int num_splits, void* workspace, size_t workspace_bytes,
+                     cram_stream_t stream);
+
+/*
+ * Answer-token logits (replaces the full-vocab lm_head + gather of
+ * re_weighting.py:159-160,169-170):  out[i] = sum_d hidden[i][d] * w_lm[ids[i]][d]
+ * in fp32; round_bf16 != 0 rounds each logit to bf16 first (transformers 5.15 bf16 logits).
+ *   hidden : bf16 [n][D] row stride h_rs;  w_lm : bf16 [V][D] row stride w_rs;  ids : int32 [n]
+ */
+int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64_t w_rs,
+                       const int32_t* ids, int n, int D, int round_bf16, float* out,
+                       cram_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CRAM_ATTN_H */

@@ -1,0 +1,138 @@
+"""Kernel parity: HIP attention / answer-logit kernels vs the CPU oracle (float64).
+
+The oracle builds the reference hook's dense [1, H, T, S] mask
+(re_weighting.py:36-61) and runs softmax attention in float64; the HIP kernels
+take the O(S) bias vector instead.  bf16 inputs, fp32 accumulation, bf16 output:
+tolerance |err| <= 2e-2 + 2e-2 |ref| elementwise and mean |err| <= 2e-3.
+"""
+import math
+
+import pytest
+import torch
+
+from oracle import hook_ref
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL, MEAN_TOL = 2e-2, 2e-2, 2e-3
+
+
+def _bias_inputs(B, Hq, S, W, gen, spans_scores=((3, 40, 0.1), (41, 90, 0.0), (91, 150, 1.0), (151, 200, 0.5))):
+    w = torch.ones((B, W), dtype=torch.float16)
+    for (a, b, sc) in spans_scores:
+        if a < W:
+            w[:, a:min(b, W - 1) + 1] = sc
+    lw = hook_ref.log_weight(w)                        # fp16 log, as the hook computes it
+    bias = lw.to(torch.bfloat16).float()               # the value the hook writes (bf16 model)
+    heads = [sorted(torch.randperm(Hq, generator=gen)[: max(1, Hq // 2)].tolist()) for _ in range(B)]
+    enable = torch.zeros((B, Hq), dtype=torch.uint8)
+    for b, hs in enumerate(heads):
+        enable[b, hs] = 1
+    return lw, bias, enable, heads
+
+
+def _check(out, ref):
+    out = out.double().cpu()
+    assert torch.isfinite(out).all()
+    err = (out - ref).abs()
+    bad = err > ATOL + RTOL * ref.abs()
+    assert not bad.any(), f"max err {err.max().item():.3e} at {bad.nonzero()[0].tolist()}"
+    assert err.mean().item() < MEAN_TOL, f"mean err {err.mean().item():.3e}"
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,T,d", [
+    (1, 4, 1, 1, 128), (1, 4, 2, 17, 128), (2, 8, 2, 128, 128), (1, 4, 4, 300, 128),
+    (1, 8, 2, 900, 128), (1, 7, 1, 257, 128), (2, 4, 1, 200, 64), (1, 32, 8, 130, 128),
+])
+@pytest.mark.parametrize("biased", [False, True])
+def test_prefill_matches_oracle(gpu_device, B, Hq, Hkv, T, d, biased):
+    gen = torch.Generator().manual_seed(1000 * T + 10 * Hq + d + biased)
+    S = T
+    # q laid out like transformers' transposed view: physical [B, T, Hq, d]
+    q = torch.randn(B, T, Hq, d, generator=gen).to(torch.bfloat16).transpose(1, 2)
+    k = torch.randn(B, Hkv, S, d, generator=gen).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, S, d, generator=gen).to(torch.bfloat16)
+    scale = 1.0 / math.sqrt(d)
+    W = max(1, S - 3)
+    if biased:
+        lw, bias, enable, heads = _bias_inputs(B, Hq, S, W, gen)
+    else:
+        lw = bias = enable = heads = None
+    ref = hook_ref.biased_attention_ref(q, k, v, lw, heads, scale)
+    from cram_amd import ops
+    dev = gpu_device
+    out = ops.attn_prefill(q.to(dev), k.to(dev), v.to(dev), scale=scale,
+                           bias=None if bias is None else bias.to(dev),
+                           enable=None if enable is None else enable.to(dev), W=W if biased else 0)
+    torch.cuda.synchronize()
+    _check(out, ref)
+
+
+def test_prefill_query_offset(gpu_device):
+    """q_len < S (queries start at q_pos0 = S - Tq), as in chunked prefill / cached suffix."""
+    gen = torch.Generator().manual_seed(7)
+    B, Hq, Hkv, S, T, d = 1, 8, 2, 333, 45, 128
+    q = torch.randn(B, Hq, T, d, generator=gen).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, S, d, generator=gen).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, S, d, generator=gen).to(torch.bfloat16)
+    lw, bias, enable, heads = _bias_inputs(B, Hq, S, 250, gen)
+    ref = hook_ref.biased_attention_ref(q, k, v, lw, heads, d ** -0.5)
+    from cram_amd import ops
+    dev = gpu_device
+    out = ops.attn_prefill(q.to(dev), k.to(dev), v.to(dev), scale=d ** -0.5, bias=bias.to(dev),
+                           enable=enable.to(dev), W=250)
+    torch.cuda.synchronize()
+    _check(out, ref)
+
+
+@pytest.mark.parametrize("B,Hq,Hkv,S,d,splits", [
+    (1, 4, 1, 1, 128, 1), (1, 32, 8, 900, 128, 1), (3, 32, 8, 900, 128, 4), (2, 28, 4, 777, 128, 3),
+    (2, 4, 4, 513, 128, 1), (1, 16, 2, 2049, 128, 8), (2, 8, 4, 300, 64, 2), (1, 8, 1, 64, 128, 2),
+])
+@pytest.mark.parametrize("ragged", [False, True])
+def test_decode_matches_oracle(gpu_device, B, Hq, Hkv, S, d, splits, ragged):
+    gen = torch.Generator().manual_seed(S * 31 + Hq + splits + ragged)
+    q = torch.randn(B, Hq, d, generator=gen).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, S + 5, d, generator=gen).to(torch.bfloat16)   # padded cache (S_max > S)
+    v = torch.randn(B, Hkv, S + 5, d, generator=gen).to(torch.bfloat16)
+    lens = [S if not ragged else max(1, S - 7 * b) for b in range(B)]
+    W = max(1, S - 2)
+    lw, bias, enable, heads = _bias_inputs(B, Hq, S, W, gen)
+    refs = []
+    for b in range(B):
+        L = lens[b]
+        Wb = min(W, L)
+        refs.append(hook_ref.biased_attention_ref(q[b:b + 1, :, None], k[b:b + 1, :, :L], v[b:b + 1, :, :L],
+                                                  lw[b:b + 1, :Wb], [heads[b]], d ** -0.5)[:, 0])
+    ref = torch.cat(refs, 0)
+    from cram_amd import ops
+    dev = gpu_device
+    out = ops.attn_decode(q.to(dev), k.to(dev), v.to(dev), scale=d ** -0.5,
+                          seq_lens=torch.tensor(lens, dtype=torch.int32, device=dev),
+                          bias=bias.to(dev), enable=enable.to(dev), W=W, num_splits=splits)
+    torch.cuda.synchronize()
+    _check(out, ref)
+
+
+def test_answer_logits(gpu_device):
+    gen = torch.Generator().manual_seed(3)
+    n, D, V = 37, 4096, 1000
+    h = torch.randn(n, D, generator=gen).to(torch.bfloat16)
+    w = (torch.randn(V, D, generator=gen) * 0.02).to(torch.bfloat16)
+    ids = torch.randint(0, V, (n,), generator=gen, dtype=torch.int32)
+    ref = (h.double() * w[ids.long()].double()).sum(-1)
+    from cram_amd import ops
+    dev = gpu_device
+    out = ops.answer_logits(h.to(dev), w.to(dev), ids.to(dev))
+    torch.cuda.synchronize()
+    assert torch.allclose(out.double().cpu(), ref, atol=1e-3, rtol=1e-4)
+    out16 = ops.answer_logits(h.to(dev), w.to(dev), ids.to(dev), round_bf16=True)
+    assert torch.equal(out16.cpu(), out.cpu().to(torch.bfloat16).float())
+
+
+def test_rejects_bad_alignment(gpu_device):
+    from cram_amd import ops
+    dev = gpu_device
+    q = torch.randn(1, 2, 4, 100, device=dev).to(torch.bfloat16)   # d = 100 unsupported
+    with pytest.raises(RuntimeError):
+        ops.attn_prefill(q, q[:, :1], q[:, :1], scale=0.1)

@@ -1,0 +1,84 @@
+"""Tiny random-weight Llama-3 / Qwen2 models with deterministic, documented weights.
+
+No checkpoint is committed.  Every parameter tensor is drawn from numpy's PCG64
+stream seeded with SeedSequence([seed, crc32(parameter name)]) (stable across
+numpy versions and machines), scaled by a per-kind std, then rounded to bf16.
+The golden vectors in tests/golden/ were produced by the reference running on
+exactly these weights, so any machine can rebuild the same model.
+"""
+from __future__ import annotations
+
+import os
+import zlib
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOK_DIR = {"llama3": os.path.join(REPO, "data", "tok_llama3"), "qwen2": os.path.join(REPO, "data", "tok_qwen")}
+DIR_NAME = {"llama3": "Llama-3-tiny", "qwen2": "Qwen2-tiny"}   # names select the reference's chat branch
+
+SPECS = {
+    "llama3": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=4, num_attention_heads=4,
+                   num_key_value_heads=2, head_dim=128, rope_theta=500000.0, rms_norm_eps=1e-5,
+                   max_position_embeddings=4096, tie_word_embeddings=False),
+    "qwen2": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=3, num_attention_heads=2,
+                  num_key_value_heads=1, rope_theta=1000000.0, rms_norm_eps=1e-6,
+                  max_position_embeddings=4096, tie_word_embeddings=False),
+}
+SEED = 20250404
+LIN_STD = 0.08
+
+
+def _draw(name: str, shape, std: float, mean: float = 0.0, seed: int = SEED) -> torch.Tensor:
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, zlib.crc32(name.encode())])))
+    a = rng.standard_normal(size=shape, dtype=np.float32) * np.float32(std) + np.float32(mean)
+    return torch.from_numpy(a).to(torch.bfloat16)
+
+
+def tokenizer(kind: str):
+    from transformers import AutoTokenizer
+    return AutoTokenizer.from_pretrained(TOK_DIR[kind])
+
+
+def config(kind: str):
+    from transformers import LlamaConfig, Qwen2Config
+    tok = tokenizer(kind)
+    spec = dict(SPECS[kind])
+    if kind == "llama3":
+        cfg = LlamaConfig(vocab_size=len(tok), bos_token_id=tok.bos_token_id, eos_token_id=tok.eos_token_id,
+                          **spec)
+    else:
+        cfg = Qwen2Config(vocab_size=len(tok), eos_token_id=tok.eos_token_id, **spec)
+    cfg.torch_dtype = torch.bfloat16
+    return cfg
+
+
+def build_model(kind: str, attn_implementation: str = "sdpa"):
+    """The tiny model on CPU in bf16 with the deterministic weights."""
+    from transformers import AutoModelForCausalLM
+    cfg = config(kind)
+    model = AutoModelForCausalLM.from_config(cfg, attn_implementation=attn_implementation, dtype=torch.bfloat16)
+    sd = {}
+    for name, p in model.state_dict().items():
+        if name.endswith("norm.weight") or "layernorm" in name:
+            sd[name] = _draw(name, tuple(p.shape), 0.1, 1.0)
+        elif name.endswith("embed_tokens.weight"):
+            sd[name] = _draw(name, tuple(p.shape), 1.0)
+        elif name.endswith(".bias"):
+            sd[name] = _draw(name, tuple(p.shape), 0.05)
+        else:
+            sd[name] = _draw(name, tuple(p.shape), LIN_STD)
+    model.load_state_dict(sd)
+    model.eval()
+    return model
+
+
+def save_model(kind: str, root: str) -> str:
+    """Write the tiny model + tokenizer as a local HF directory (name selects the chat branch)."""
+    path = os.path.join(root, DIR_NAME[kind])
+    if not os.path.exists(os.path.join(path, "config.json")):
+        os.makedirs(path, exist_ok=True)
+        build_model(kind).save_pretrained(path)
+        tokenizer(kind).save_pretrained(path)
+    return path
