@@ -1,0 +1,368 @@
+"""CrAMEngine: Llama-3 / Qwen2-family forward on MI355X built around the HIP attention kernels.
+
+The reference runs the model through transformers with a dense-mask hook
+(re_weighting.py:116-138 generate path, :152-175 IE path).  The engine runs the
+same network (weights taken from a transformers model, or random-init of the
+same shapes for throughput runs) with:
+  * fused QKV and gate/up projections (one hipBLASLt GEMM each, via torch),
+  * credibility-biased attention from libcram_attn (prefill MFMA kernel,
+    decode split-S kernel) reading q/k/v straight out of the QKV buffer,
+  * a static per-batch KV cache ([L][B][Hkv][S_max][d], bf16) and a decode
+    step whose attention reads per-row lengths from device memory, so a whole
+    greedy step can be captured in one hipGraph and replayed,
+  * answer-token logits by the fp32 gather kernel instead of the full-vocab
+    lm_head (IE sweep).
+Elementwise ops follow transformers' exact op order and rounding points
+(LlamaRMSNorm, apply_rotary_pos_emb, LlamaMLP) so the engine tracks the
+reference numerics; only GEMM reduction order and the attention kernel differ.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .bias import CredibilityBias
+
+
+@dataclass
+class ModelSpec:
+    num_layers: int
+    hidden: int
+    num_heads: int
+    num_kv_heads: int
+    head_dim: int
+    intermediate: int
+    vocab: int
+    eps: float
+    qkv_bias: bool
+    family: str = "llama"
+
+    @property
+    def q_size(self):
+        return self.num_heads * self.head_dim
+
+    @property
+    def kv_size(self):
+        return self.num_kv_heads * self.head_dim
+
+    @staticmethod
+    def from_config(cfg) -> "ModelSpec":
+        hd = getattr(cfg, "head_dim", None) or cfg.hidden_size // cfg.num_attention_heads
+        fam = "qwen2" if cfg.model_type.startswith("qwen2") else "llama"
+        return ModelSpec(cfg.num_hidden_layers, cfg.hidden_size, cfg.num_attention_heads,
+                         getattr(cfg, "num_key_value_heads", cfg.num_attention_heads), hd, cfg.intermediate_size,
+                         cfg.vocab_size, cfg.rms_norm_eps, fam == "qwen2" or bool(getattr(cfg, "attention_bias", False)),
+                         fam)
+
+    # the shapes BASELINE.json names
+    @staticmethod
+    def llama3_8b() -> "ModelSpec":
+        return ModelSpec(32, 4096, 32, 8, 128, 14336, 128256, 1e-5, False, "llama")
+
+    @staticmethod
+    def qwen2_7b() -> "ModelSpec":
+        return ModelSpec(28, 3584, 28, 4, 128, 18944, 152064, 1e-6, True, "qwen2")
+
+    def layer_flops(self, T: int) -> float:
+        """GEMM flops of one decoder layer over T tokens (2 * params * T)."""
+        p = self.hidden * (self.q_size + 2 * self.kv_size) + self.q_size * self.hidden + 3 * self.hidden * self.intermediate
+        return 2.0 * p * T
+
+
+class LayerW:
+    __slots__ = ("ln1", "wqkv", "bqkv", "wo", "ln2", "wgu", "wd")
+
+
+class CrAMEngine:
+    def __init__(self, spec: ModelSpec, layers: List[LayerW], embed: torch.Tensor, norm: torch.Tensor,
+                 lm_head: torch.Tensor, inv_freq: torch.Tensor, attn_scaling: float = 1.0):
+        self.spec = spec
+        self.layers = layers
+        self.embed = embed
+        self.norm = norm
+        self.lm_head = lm_head
+        self.inv_freq = inv_freq.float()
+        self.attn_scaling = float(attn_scaling)
+        self.device = embed.device
+        self.dtype = embed.dtype
+        self.scale = spec.head_dim ** -0.5
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def from_hf(model) -> "CrAMEngine":
+        """Share the transformers model's weights (q/k/v and gate/up are concatenated once)."""
+        spec = ModelSpec.from_config(model.config)
+        base = model.model
+        layers = []
+        for blk in base.layers:
+            a, m = blk.self_attn, blk.mlp
+            lw = LayerW()
+            lw.ln1 = blk.input_layernorm.weight.data
+            lw.wqkv = torch.cat([a.q_proj.weight.data, a.k_proj.weight.data, a.v_proj.weight.data], 0).contiguous()
+            lw.bqkv = (torch.cat([a.q_proj.bias.data, a.k_proj.bias.data, a.v_proj.bias.data], 0).contiguous()
+                       if a.q_proj.bias is not None else None)
+            lw.wo = a.o_proj.weight.data
+            lw.ln2 = blk.post_attention_layernorm.weight.data
+            lw.wgu = torch.cat([m.gate_proj.weight.data, m.up_proj.weight.data], 0).contiguous()
+            lw.wd = m.down_proj.weight.data
+            layers.append(lw)
+        rot = base.rotary_emb
+        return CrAMEngine(spec, layers, base.embed_tokens.weight.data, base.norm.weight.data,
+                          model.lm_head.weight.data, rot.inv_freq.detach().to(model.device),
+                          getattr(rot, "attention_scaling", 1.0))
+
+    @staticmethod
+    def random(spec: ModelSpec, device, seed: int = 0, std: float = 0.02, rope_theta: float = 500000.0,
+               dtype=torch.bfloat16) -> "CrAMEngine":
+        """Random-init weights of the given architecture (throughput runs; no checkpoint offline)."""
+        g = torch.Generator(device=device).manual_seed(seed)
+
+        def rnd(*shape, s=std):
+            return (torch.randn(*shape, generator=g, device=device, dtype=torch.float32) * s).to(dtype)
+
+        def ones_ish(n):
+            return (1.0 + 0.05 * torch.randn(n, generator=g, device=device)).to(dtype)
+
+        layers = []
+        for _ in range(spec.num_layers):
+            lw = LayerW()
+            lw.ln1 = ones_ish(spec.hidden)
+            lw.wqkv = rnd(spec.q_size + 2 * spec.kv_size, spec.hidden)
+            lw.bqkv = rnd(spec.q_size + 2 * spec.kv_size) if spec.qkv_bias else None
+            lw.wo = rnd(spec.hidden, spec.q_size)
+            lw.ln2 = ones_ish(spec.hidden)
+            lw.wgu = rnd(2 * spec.intermediate, spec.hidden)
+            lw.wd = rnd(spec.hidden, spec.intermediate)
+            layers.append(lw)
+        embed = rnd(spec.vocab, spec.hidden, s=1.0)
+        lm_head = rnd(spec.vocab, spec.hidden)
+        inv_freq = 1.0 / (rope_theta ** (torch.arange(0, spec.head_dim, 2, dtype=torch.float32, device=device)
+                                         / spec.head_dim))
+        return CrAMEngine(spec, layers, embed, ones_ish(spec.hidden), lm_head, inv_freq)
+
+    # ------------------------------------------------------------------ elementwise (transformers op order)
+    def rmsnorm(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        xf = x.float()
+        var = xf.pow(2).mean(-1, keepdim=True)
+        return w * (xf * torch.rsqrt(var + self.spec.eps)).to(x.dtype)
+
+    def rope_tables(self, pos: torch.Tensor):
+        """pos int64 [..., T] -> cos, sin [..., T, d] in the model dtype (LlamaRotaryEmbedding.forward)."""
+        freqs = pos.float()[..., None] * self.inv_freq
+        emb = torch.cat((freqs, freqs), dim=-1)
+        return (emb.cos() * self.attn_scaling).to(self.dtype), (emb.sin() * self.attn_scaling).to(self.dtype)
+
+    @staticmethod
+    def _rotate_half(x):
+        h = x.shape[-1] // 2
+        return torch.cat((-x[..., h:], x[..., :h]), dim=-1)
+
+    def rope(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+        """x [..., T, H, d]; cos/sin [..., T, d] (apply_rotary_pos_emb, unsqueeze over heads)."""
+        c, s = cos.unsqueeze(-2), sin.unsqueeze(-2)
+        return (x * c) + (self._rotate_half(x) * s)
+
+    def mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
+        gu = F.linear(x, lw.wgu)
+        Fi = self.spec.intermediate
+        return F.linear(F.silu(gu[..., :Fi]) * gu[..., Fi:], lw.wd)
+
+    def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin):
+        """x [..., T, D] -> q [..., T, Hq, d], k, v [..., T, Hkv, d] (roped)."""
+        sp = self.spec
+        y = F.linear(x, lw.wqkv, lw.bqkv)
+        q = y[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
+        k = y[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
+        v = y[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
+        return self.rope(q, cos, sin), self.rope(k, cos, sin), v
+
+    # ------------------------------------------------------------------ prefill / full forward
+    def attention(self, q, k, v, bias: Optional[torch.Tensor] = None, enable: Optional[torch.Tensor] = None,
+                  W: int = 0) -> torch.Tensor:
+        """q [B, Tq, Hq, d], k/v [B, S, Hkv, d] (token-major views) -> [B, Tq, Hq, d]."""
+        return ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale,
+                                bias=bias, enable=enable, W=W)
+
+    def layer(self, h: torch.Tensor, l: int, cos, sin, bias=None, enable=None, W: int = 0,
+              out_rows: Optional[int] = None, kv_out=None) -> torch.Tensor:
+        """One decoder layer over h [B, T, D].  out_rows=n computes attention/MLP for the last n rows only."""
+        lw = self.layers[l]
+        x = self.rmsnorm(h, lw.ln1)
+        q, k, v = self.qkv(x, lw, cos, sin)
+        if kv_out is not None:
+            kv_out(l, k, v)
+        if out_rows is not None:
+            q = q[:, -out_rows:]
+            h = h[:, -out_rows:]
+        a = self.attention(q, k, v, bias, enable, W)
+        h = h + F.linear(a.flatten(-2), lw.wo)
+        return h + self.mlp(self.rmsnorm(h, lw.ln2), lw)
+
+    def positions(self, B: int, T: int, start: int = 0) -> torch.Tensor:
+        return torch.arange(start, start + T, device=self.device)[None].expand(B, T)
+
+    @torch.no_grad()
+    def forward_hidden(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None, out_rows: Optional[int] = None,
+                       kv_out=None, layer_hook=None) -> torch.Tensor:
+        """ids [B, T] -> final-norm hidden states [B, T or out_rows, D]."""
+        B, T = ids.shape
+        cos, sin = self.rope_tables(self.positions(B, T))
+        h = self.embed[ids]
+        L = self.spec.num_layers
+        for l in range(L):
+            if layer_hook is not None:
+                layer_hook(l, h)
+            en = cb.enable[l] if cb is not None else None
+            h = self.layer(h, l, cos, sin, cb.bias if cb is not None else None, en, cb.W if cb is not None else 0,
+                           out_rows=out_rows if l == L - 1 else None, kv_out=kv_out)
+        return self.rmsnorm(h, self.norm)
+
+    @torch.no_grad()
+    def logits(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None, last: Optional[int] = None):
+        h = self.forward_hidden(ids, cb, out_rows=last)
+        return F.linear(h, self.lm_head)
+
+    def answer_logits(self, hidden: torch.Tensor, ids: torch.Tensor, round_bf16: bool = False) -> torch.Tensor:
+        """hidden [n, D] bf16, ids int32 [n] -> fp32 [n] (HIP gather-dot)."""
+        return ops.answer_logits(hidden.contiguous(), self.lm_head, ids, round_bf16=round_bf16)
+
+    # ------------------------------------------------------------------ batched greedy decode
+    @torch.no_grad()
+    def generate(self, prompts: Sequence[torch.Tensor], weights16: Sequence[torch.Tensor], layers_to_heads: dict,
+                 max_new_tokens: int = 100, eos_ids: Sequence[int] = (), bad_token_ids: Sequence[int] = (),
+                 use_graph: bool = True, stop_on_eos: bool = True) -> List[List[int]]:
+        """Greedy decode of several prompts at once (per-row lengths, per-row credibility bias).
+
+        Returns the generated ids of every prompt, truncated after its first EOS
+        (tokens generated after EOS are never observed, so per-row results equal
+        one-at-a-time generation as in re_weighting.py:127-132).
+        """
+        sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids)
+        sess.prefill()
+        steps = max_new_tokens - 1
+        if use_graph and steps > 0:
+            sess.capture()
+        eos = torch.tensor(list(eos_ids) or [-1], device=self.device)
+        done_at = None
+        for t in range(steps):
+            sess.step(use_graph)
+            if stop_on_eos and eos_ids and (t % 8 == 7 or t == steps - 1):
+                gen = sess.generated()
+                hit = torch.isin(gen, eos).any(1)
+                if bool(hit.all()):
+                    done_at = t
+                    break
+        del done_at
+        out = []
+        gen = sess.generated().cpu().tolist()
+        for row in gen:
+            row = row[:max_new_tokens]
+            if eos_ids:
+                for i, tok in enumerate(row):
+                    if tok in eos_ids:
+                        row = row[:i + 1]
+                        break
+            out.append(row)
+        return out
+
+
+class DecodeSession:
+    """Static-shape state of one batched greedy decode (KV cache, bias, token buffers)."""
+
+    def __init__(self, eng: CrAMEngine, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids=()):
+        sp = eng.spec
+        self.eng = eng
+        self.B = len(prompts)
+        self.lens = [int(p.numel()) for p in prompts]
+        self.S_max = max(self.lens) + max_new_tokens
+        self.S_max = (self.S_max + 63) // 64 * 64
+        dev = eng.device
+        self.prompts = [p.reshape(-1).to(dev) for p in prompts]
+        self.cb = CredibilityBias.build(list(weights16), layers_to_heads, sp.num_layers, sp.num_heads, dev,
+                                        eng.dtype, s_cap=self.S_max)
+        self.k_cache = torch.zeros((sp.num_layers, self.B, sp.num_kv_heads, self.S_max, sp.head_dim),
+                                   dtype=eng.dtype, device=dev)
+        self.v_cache = torch.zeros_like(self.k_cache)
+        self.max_new = max_new_tokens
+        self.tokens = torch.zeros(self.B, dtype=torch.long, device=dev)
+        self.pos = torch.tensor(self.lens, dtype=torch.long, device=dev)          # position of the token being fed
+        self.seq_lens = torch.tensor(self.lens, dtype=torch.int32, device=dev)     # keys visible after the write
+        self.out = torch.zeros((self.B, max_new_tokens), dtype=torch.long, device=dev)
+        self.t = torch.zeros((), dtype=torch.long, device=dev)                    # next output column
+        self.bad = torch.tensor(list(bad_token_ids), dtype=torch.long, device=dev) if bad_token_ids else None
+        splits = max(1, min(16, math.ceil(512 / max(1, self.B * sp.num_kv_heads))))
+        self.splits = max(1, min(splits, self.S_max // 256))
+        self.ws = (torch.empty(ops.decode_workspace_bytes(self.B, sp.num_heads, sp.head_dim, self.splits),
+                               dtype=torch.uint8, device=dev) if self.splits > 1 else None)
+        self.graph = None
+        self.rows = torch.arange(self.B, device=dev)
+
+    def _pick(self, logits: torch.Tensor) -> torch.Tensor:
+        if self.bad is not None:
+            logits = logits.index_fill(-1, self.bad, float("-inf"))
+        return torch.argmax(logits, dim=-1)
+
+    def prefill(self):
+        eng = self.eng
+        for b, ids in enumerate(self.prompts):
+            T = ids.numel()
+
+            def kv_out(l, k, v, b=b, T=T):
+                self.k_cache[l, b, :, :T] = k[0].transpose(0, 1)
+                self.v_cache[l, b, :, :T] = v[0].transpose(0, 1)
+
+            sub = CredibilityBias(self.cb.bias[b:b + 1], self.cb.enable[:, b:b + 1], self.cb.W)
+            h = eng.forward_hidden(ids[None], sub, out_rows=1, kv_out=kv_out)
+            self.tokens[b] = self._pick(F.linear(h[0, -1], eng.lm_head))
+        self.out[:, 0] = self.tokens
+        self.t.fill_(1)
+
+    def _step_body(self):
+        eng, sp = self.eng, self.eng.spec
+        cos, sin = eng.rope_tables(self.pos[:, None])            # [B, 1, d]
+        h = eng.embed[self.tokens][:, None]                      # [B, 1, D]
+        self.seq_lens.add_(1)
+        for l, lw in enumerate(eng.layers):
+            x = eng.rmsnorm(h, lw.ln1)
+            q, k, v = eng.qkv(x, lw, cos, sin)
+            self.k_cache[l, self.rows, :, self.pos] = k[:, 0]
+            self.v_cache[l, self.rows, :, self.pos] = v[:, 0]
+            a = ops.attn_decode(q[:, 0], self.k_cache[l], self.v_cache[l], scale=eng.scale, seq_lens=self.seq_lens,
+                                bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
+                                workspace=self.ws)
+            h = h + F.linear(a.flatten(-2)[:, None], lw.wo)
+            h = h + eng.mlp(eng.rmsnorm(h, lw.ln2), lw)
+        hn = eng.rmsnorm(h[:, 0], eng.norm)
+        nxt = self._pick(F.linear(hn, eng.lm_head))
+        self.tokens.copy_(nxt)
+        self.out.index_copy_(1, self.t.view(1), nxt[:, None])
+        self.t.add_(1)
+        self.pos.add_(1)
+
+    def capture(self):
+        s = torch.cuda.Stream(self.eng.device)
+        s.wait_stream(torch.cuda.current_stream(self.eng.device))
+        # warm the allocator / kernels on a side stream, then restore the state it advanced
+        snap = (self.tokens.clone(), self.pos.clone(), self.seq_lens.clone(), self.t.clone(), self.out.clone())
+        with torch.cuda.stream(s):
+            self._step_body()
+        torch.cuda.current_stream(self.eng.device).wait_stream(s)
+        self.tokens.copy_(snap[0]); self.pos.copy_(snap[1]); self.seq_lens.copy_(snap[2])
+        self.t.copy_(snap[3]); self.out.copy_(snap[4])
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._step_body()
+
+    def step(self, use_graph=True):
+        if use_graph and self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step_body()
+
+    def generated(self) -> torch.Tensor:
+        return self.out

@@ -1,0 +1,104 @@
+"""IE-sweep drivers and influential-head ranking (utils/find_best_heads.py, same file formats).
+
+  casual_tracing_per_head       find_best_heads.py:13-58   per-question IE grid, resume by skipping
+  casual_tracing_per_head_with_position  :61-110          fake passage moved through positions 0..4
+  casual_tracing_combine_all    :113-132                   mean over questions, ranking
+  find_top_k_heads              :135-150                   top-k -> {layer: [heads]}
+
+Ranking tie-break: the reference uses np.argsort(flat)[::-1] (quicksort, so the
+order of exactly-equal means depends on the numpy version).  Here the order is
+fixed: value descending, then flat index (layer*H + head) DESCENDING — which is
+what a stable ascending sort reversed yields, and what the reference's
+fixtures show for the tied pairs we checked (tests/test_ranking.py).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+
+def rank_heads(heads_scores) -> List[Tuple[float, Tuple[int, int]]]:
+    """[Nq, L, H] (or [L, H]) IE -> [(mean IE, (layer, head))] sorted, deterministic tie-break."""
+    a = np.asarray(heads_scores, dtype=np.float64)
+    mean = a.mean(axis=0) if a.ndim == 3 else a
+    flat = mean.reshape(-1)
+    order = np.argsort(flat, kind="stable")[::-1]
+    L, H = mean.shape
+    return [(float(flat[i]), (int(i // H), int(i % H))) for i in order]
+
+
+def top_k(ranked: Sequence[Tuple[float, Tuple[int, int]]], k: int) -> Dict[int, List[int]]:
+    out: Dict[int, List[int]] = {}
+    for _, (l, h) in ranked[:k]:
+        out.setdefault(l, []).append(h)
+    return out
+
+
+def casual_tracing_combine_all(input_path: str) -> list:
+    with open(os.path.join(input_path, "heads_scores.json"), encoding="utf-8") as f:
+        data = json.load(f)
+    ranked = rank_heads(data)
+    with open(os.path.join(input_path, "heads_scores_mean.json"), "w", encoding="utf-8") as f:
+        json.dump([(v, list(lh)) for v, lh in ranked], f, ensure_ascii=False, indent=4)
+    return ranked
+
+
+def find_top_k_heads(input_path: str, topk: int = 10) -> Dict[int, List[int]]:
+    with open(os.path.join(input_path, "heads_scores_mean.json"), encoding="utf-8") as f:
+        data = json.load(f)
+    sel: Dict[int, List[int]] = {}
+    for _, (l, h) in data[:topk]:
+        sel.setdefault(l, []).append(h)
+    with open(os.path.join(input_path, "selected_heads.json"), "w", encoding="utf-8") as f:
+        json.dump(sel, f, ensure_ascii=False, indent=4)
+    return sel
+
+
+def sweep_contexts(sample: dict, contexts_type=("ori_fake", "reranked_dense"), topk: int = 4):
+    """find_best_heads.py:41-48: contexts and the sweep scores [0] + [1]*4."""
+    contexts, scores = [], []
+    if "ori_fake" in contexts_type:
+        contexts.extend(sample["ori_fake"])
+        scores.extend([0])
+    if "reranked_dense" in contexts_type:
+        contexts.extend(sample["reranked_dense_ctxs"][:topk])
+        scores.extend([1, 1, 1, 1])
+    return contexts, scores
+
+
+def casual_tracing_per_head(data: list, model, output_file: str, contexts_type=("ori_fake", "reranked_dense"),
+                            topk: int = 4) -> list:
+    """Per-question IE grids appended to output_file, resuming after the questions already present."""
+    done = []
+    if os.path.exists(output_file):
+        with open(output_file, encoding="utf-8") as f:
+            done = json.load(f)
+    for idx, sample in enumerate(data):
+        if idx < len(done):
+            continue
+        ctx, sc = sweep_contexts(sample, contexts_type, topk)
+        wrong = sample.get("wrong answer", sample.get("wrong_answer"))
+        done.append(model.cal_logits(question=sample["question"], paras=ctx, scores=sc, wrong_answer=wrong))
+        os.makedirs(os.path.dirname(os.path.abspath(output_file)), exist_ok=True)
+        with open(output_file, "w", encoding="utf-8") as f:
+            json.dump(done, f, ensure_ascii=False, indent=4)
+    return done
+
+
+def casual_tracing_per_head_with_position(data: list, model, topk: int = 4) -> list:
+    """find_best_heads.py:61-110: the fake passage at positions 0..4 among the 4 retrieved ones."""
+    res = []
+    for sample in data:
+        fake = sample["ori_fake"]
+        docs = sample["reranked_dense_ctxs"][:topk]
+        wrong = sample.get("wrong answer", sample.get("wrong_answer"))
+        per_pos = []
+        for pos in range(5):
+            ctx = docs[:pos] + list(fake) + docs[pos:]
+            sc = [1] * pos + [0] + [1] * (4 - pos)
+            per_pos.append(model.cal_logits(question=sample["question"], paras=ctx, scores=sc, wrong_answer=wrong))
+        res.append(per_pos)
+    return res

@@ -1,0 +1,175 @@
+"""Drop-in replacements for the reference's Re_Weighting_Strategy and Find_Best_Heads.
+
+Same constructor / method names, argument meaning, return types and quirks as
+/root/reference/utils/re_weighting.py (cited per method), with two deliberate
+differences:
+  * `model_name` must be a LOCAL model directory (there is no hub access); its
+    name still selects the chat branch ("Llama-3" / "Qwen" substrings);
+  * the dense-mask forward-pre-hooks are replaced by the "cram_hip" attention
+    implementation (fused HIP kernels, O(S) bias), and cal_logits runs the
+    head-batched IE sweep (cram_amd.sweep) instead of 1 + L*H full forwards.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from . import attention as _attn
+from . import spans as _spans
+from .bias import CredibilityBias, all_heads
+from .engine import CrAMEngine
+from . import sweep as _sweep
+
+
+class Re_Weighting_Strategy:
+    """re_weighting.py:22-138."""
+
+    def __init__(self, model_name: str = "Llama-2-13b-chat-hf", layers_to_be_modified: dict = None,
+                 bad_words_ids=None, device: str = "cuda:0"):
+        # re_weighting.py:24-34
+        from transformers import AutoModelForCausalLM, AutoTokenizer
+        _attn.register()
+        self.device = torch.device(device)
+        self.tokenizer = AutoTokenizer.from_pretrained(model_name)
+        self.model = AutoModelForCausalLM.from_pretrained(model_name, dtype="auto",
+                                                          attn_implementation=_attn.IMPL_NAME).to(self.device)
+        self.model.eval()
+        self.model_name = model_name
+        self.bad_words_ids = list(bad_words_ids or [])
+        self.num_hidden_layers = self.model.config.num_hidden_layers
+        self.model_num_attention_heads = self.model.config.num_attention_heads
+        if not layers_to_be_modified:
+            layers_to_be_modified = all_heads(self.num_hidden_layers, self.model_num_attention_heads)
+        self.layers_to_be_modified = layers_to_be_modified
+        self._engine: Optional[CrAMEngine] = None
+
+    @property
+    def engine(self) -> CrAMEngine:
+        if self._engine is None:
+            self._engine = CrAMEngine.from_hf(self.model)
+        return self._engine
+
+    # ------------------------------------------------------------------ reference-semantics utility
+    def edit_attention_mask(self, module, input_args: tuple, input_kwargs: dict, attention_weight: torch.Tensor,
+                            head_idx: list = ()):
+        """re_weighting.py:36-61: materialise the dense mask the reference hook would pass.
+
+        Kept for API compatibility and inspection; the HIP path never builds it.
+        """
+        hs = input_kwargs["hidden_states"]
+        dt, dev = hs.dtype, hs.device
+        W = attention_weight.shape[-1]
+        am = input_kwargs.get("attention_mask")
+        if am is None:
+            T = hs.shape[1]
+            S = int(input_kwargs["position_ids"][0][-1]) + 1
+            if T == 1:
+                am = torch.zeros((1, 1, 1, S), dtype=dt, device=dev)
+            else:
+                am = torch.full((T, S), torch.finfo(dt).min, dtype=dt, device=dev).triu(1).view(1, 1, T, S)
+        am = am.clone()
+        if am.shape[1] == 1:
+            am = am.repeat(1, self.model_num_attention_heads, 1, 1)
+        vals = attention_weight.reshape(1, 1, 1, W).to(dtype=dt, device=dev)
+        sel = torch.zeros((1, am.shape[1], 1, 1), dtype=torch.bool, device=dev)
+        for h in head_idx:
+            sel[0, h] = True
+        region = am[..., :W]
+        region.copy_(torch.where(sel & (region == 0), vals.expand_as(region), region))
+        input_kwargs["attention_mask"] = am
+        return input_args, input_kwargs
+
+    # ------------------------------------------------------------------ prompt + weights
+    def decode_with_special_attention(self, question: str = "", paras: list = (), scores: list = (),
+                                      answer: str = ""):
+        """re_weighting.py:63-113 -> (BatchEncoding on the device, fp16 weight [1, T])."""
+        _, enc, w, _ = _spans.encode(self.tokenizer, self.model_name, question, list(paras), list(scores), answer)
+        enc.pop("offset_mapping")
+        return enc.to(self.device), w.to(self.device)
+
+    def _bias(self, w16: torch.Tensor, layers_to_heads: Dict) -> CredibilityBias:
+        return CredibilityBias.build([w16.reshape(1, -1).cpu()], layers_to_heads, self.num_hidden_layers,
+                                     self.model_num_attention_heads, self.device, self.model.dtype)
+
+    def _generate_kwargs(self) -> dict:
+        kw = {"do_sample": False, "max_new_tokens": 100}
+        if self.bad_words_ids:
+            kw["bad_words_ids"] = self.bad_words_ids
+        if _spans.model_family(self.model_name) == "llama3":
+            kw["eos_token_id"] = [self.tokenizer.eos_token_id, self.tokenizer.convert_tokens_to_ids("<|eot_id|>")]
+        return kw
+
+    @torch.no_grad()
+    def run_RAG_with_attention_weighting(self, question: str = "", paras: list = (), scores: list = ()):
+        """re_weighting.py:115-138 -> (prompt, answer)."""
+        model_inputs, w = self.decode_with_special_attention(question=question, paras=paras, scores=scores)
+        cb = self._bias(w, self.layers_to_be_modified)
+        prompt = self.tokenizer.decode(model_inputs["input_ids"][0][1:])
+        with _attn.reweighting(self.model, cb):
+            outputs = self.model.generate(**model_inputs, **self._generate_kwargs())
+        output = self.tokenizer.decode(outputs[0][1:-1])          # drops the last id even if not EOS (:133)
+        output = output[output.find(prompt) + len(prompt):]
+        return prompt, output
+
+    @torch.no_grad()
+    def run_RAG_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
+                      max_new_tokens: int = 100, use_graph: bool = True) -> List[tuple]:
+        """Batched greedy decode on the engine (per-row lengths and bias); same (prompt, answer) per question."""
+        prompts, ws = [], []
+        for q, p, s in zip(questions, paras_list, scores_list):
+            enc, w = self.decode_with_special_attention(question=q, paras=p, scores=s)
+            prompts.append(enc["input_ids"][0])
+            ws.append(w.cpu())
+        kw = self._generate_kwargs()
+        eos = kw.get("eos_token_id", self.model.generation_config.eos_token_id)
+        eos = [eos] if isinstance(eos, int) else list(eos or [])
+        bad = [b[0] for b in self.bad_words_ids if len(b) == 1]
+        if len(bad) != len(self.bad_words_ids):
+            raise NotImplementedError("multi-token bad_words_ids are not supported by the batched engine")
+        gens = self.engine.generate(prompts, ws, self.layers_to_be_modified, max_new_tokens=max_new_tokens,
+                                    eos_ids=eos, bad_token_ids=bad, use_graph=use_graph)
+        res = []
+        for ids, g in zip(prompts, gens):
+            full = torch.cat([ids.cpu(), torch.tensor(g, dtype=ids.dtype)])
+            prompt = self.tokenizer.decode(ids[1:])
+            out = self.tokenizer.decode(full[1:-1])
+            res.append((prompt, out[out.find(prompt) + len(prompt):]))
+        return res
+
+
+class Find_Best_Heads(Re_Weighting_Strategy):
+    """re_weighting.py:141-175."""
+
+    def __init__(self, model_name: str = "Llama-2-13b-chat-hf", layers_to_be_modified: list = (),
+                 device: str = "cuda:0"):
+        super().__init__(model_name=model_name, device=device)
+        torch.manual_seed(42)
+        torch.cuda.manual_seed_all(42)
+        self.model_num_hidden_layers = self.model.config.num_hidden_layers
+        self.model_num_attention_heads = self.model.config.num_attention_heads
+        self.hidden_size = self.model.config.hidden_size
+
+    def answer_ids(self, wrong_answer: str) -> torch.Tensor:
+        """re_weighting.py:155: standalone tokenisation, first id dropped (also for tokenizers without BOS)."""
+        return self.tokenizer([wrong_answer], return_tensors="pt")["input_ids"][0, 1:]
+
+    @torch.no_grad()
+    def cal_logits_tensor(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
+                          wrong_answer: str = "my name is", round_bf16_logits: bool = False) -> torch.Tensor:
+        """IE [L, H] fp32 on the device (no host sync)."""
+        ans = self.answer_ids(wrong_answer)
+        model_inputs, w = self.decode_with_special_attention(question=question, paras=paras, scores=scores,
+                                                             answer=wrong_answer)
+        L, H = self.model_num_hidden_layers, self.model_num_attention_heads
+        if ans.numel() == 0:   # the reference sums an empty selection: IE == 0 everywhere
+            return torch.zeros((L, H), dtype=torch.float32, device=self.device)
+        return _sweep.ie_question(self.engine, model_inputs["input_ids"][0], w[0].cpu(), ans,
+                                  round_bf16_logits=round_bf16_logits)
+
+    def cal_logits(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
+                   wrong_answer: str = "my name is") -> list:
+        """re_weighting.py:152-175 -> list[L][H] of Python floats (IE = ori - cur)."""
+        ie = self.cal_logits_tensor(question, paras, scores, right_answer, wrong_answer)
+        return ie.double().cpu().numpy().astype(np.float64).tolist()

@@ -1,0 +1,83 @@
+"""Test-only CPU stand-ins for cram_amd.ops (host-logic tests without a GPU).
+
+They let the CPU suite exercise the engine / sweep / transformers-registration
+plumbing; the GPU suite runs the same code on the HIP kernels.  Math: fp32
+softmax attention with the same bias semantics, result rounded to bf16 like the
+kernels' output.
+"""
+import contextlib
+import math
+
+import torch
+
+
+def attn_prefill(q, k, v, *, scale, q_pos0=None, bias=None, enable=None, W=0, out=None):
+    B, Hq, Tq, d = q.shape
+    _, Hkv, S, _ = k.shape
+    if q_pos0 is None:
+        q_pos0 = S - Tq
+    G = Hq // Hkv
+    kk = k.float().repeat_interleave(G, 1)
+    vv = v.float().repeat_interleave(G, 1)
+    s = torch.matmul(q.float(), kk.transpose(-1, -2)) * scale
+    qi = torch.arange(Tq)[:, None] + q_pos0
+    kj = torch.arange(S)[None, :]
+    s = s.masked_fill(kj > qi, float("-inf"))
+    if bias is not None and enable is not None and W > 0:
+        add = torch.zeros((B, S))
+        Wc = min(W, S)
+        add[:, :Wc] = bias[:, :Wc].float().cpu()
+        en = enable.cpu().bool()[:, :, None, None]
+        add = torch.where(en, add[:, None, None, :], torch.zeros(()))
+        s = s + add
+    p = torch.softmax(s, -1)
+    o = torch.matmul(p, vv).to(q.dtype).transpose(1, 2).contiguous()
+    if out is not None:
+        out.copy_(o)
+        return out
+    return o
+
+
+def attn_decode(q, k, v, *, scale, seq_lens=None, bias=None, enable=None, W=0, num_splits=1, workspace=None,
+                out=None):
+    B, Hq, d = q.shape
+    outs = []
+    for b in range(B):
+        L = int(seq_lens[b]) if seq_lens is not None else k.shape[2]
+        o = attn_prefill(q[b:b + 1, :, None], k[b:b + 1, :, :L], v[b:b + 1, :, :L], scale=scale, q_pos0=L - 1,
+                         bias=None if bias is None else bias[b:b + 1], enable=None if enable is None else enable[b:b + 1],
+                         W=min(W, L))
+        outs.append(o[:, 0])
+    o = torch.cat(outs, 0)
+    if out is not None:
+        out.copy_(o)
+        return out
+    return o
+
+
+def answer_logits(hidden, w_lm, ids, *, round_bf16=False, out=None):
+    r = (hidden.float() * w_lm[ids.long()].float()).sum(-1)
+    if round_bf16:
+        r = r.to(torch.bfloat16).float()
+    return r
+
+
+def decode_workspace_bytes(B, Hq, d, num_splits):
+    return 0
+
+
+@contextlib.contextmanager
+def patched_ops():
+    """Route cram_amd.ops through the CPU stand-ins for the duration of a CPU test."""
+    from cram_amd import ops
+    saved = {n: getattr(ops, n) for n in ("attn_prefill", "attn_decode", "answer_logits", "decode_workspace_bytes")}
+    ops.attn_prefill, ops.attn_decode, ops.answer_logits = attn_prefill, attn_decode, answer_logits
+    ops.decode_workspace_bytes = decode_workspace_bytes
+    try:
+        yield
+    finally:
+        for n, f in saved.items():
+            setattr(ops, n, f)
+
+
+del math

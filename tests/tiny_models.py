@@ -74,11 +74,19 @@ def build_model(kind: str, attn_implementation: str = "sdpa"):
     return model
 
 
-def save_model(kind: str, root: str) -> str:
-    """Write the tiny model + tokenizer as a local HF directory (name selects the chat branch)."""
-    path = os.path.join(root, DIR_NAME[kind])
+def save_model(kind: str, root: str, fp32: bool = False) -> str:
+    """Write the tiny model + tokenizer as a local HF directory (name selects the chat branch).
+
+    fp32=True stores the same (bf16-valued) weights widened to float32: the
+    float32 reference run of that model is the IE ground truth of the tests.
+    """
+    path = os.path.join(root, DIR_NAME[kind] + ("-f32" if fp32 else ""))
     if not os.path.exists(os.path.join(path, "config.json")):
         os.makedirs(path, exist_ok=True)
-        build_model(kind).save_pretrained(path)
+        m = build_model(kind)
+        if fp32:
+            m = m.float()
+            m.config.torch_dtype = torch.float32
+        m.save_pretrained(path)
         tokenizer(kind).save_pretrained(path)
     return path
