@@ -13,6 +13,51 @@ import torch
 from . import _lib
 
 
+class KernelTimer:
+    """Optional live timing of kernel launches with HIP events on the launch stream (bench roofline).
+
+    When enabled, every launch of a named kernel is bracketed by two events on
+    torch's current stream (the stream the kernel is enqueued on) and its
+    algorithmic flops / bytes are recorded; `summary()` syncs and reduces.
+    """
+
+    def __init__(self):
+        self.enabled = False
+        self.rec = {}
+
+    def record(self, name, flops, nbytes, dev):
+        if not self.enabled:
+            return None
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record(torch.cuda.current_stream(dev))
+        self.rec.setdefault(name, []).append((s, e, float(flops), float(nbytes), dev))
+        return e
+
+    def summary(self):
+        out = {}
+        for name, rows in self.rec.items():
+            torch.cuda.synchronize()
+            ms = [s.elapsed_time(e) for s, e, *_ in rows]
+            out[name] = {"launches": len(rows), "total_ms": sum(ms), "avg_ms": sum(ms) / len(ms),
+                         "flops": sum(r[2] for r in rows), "bytes": sum(r[3] for r in rows)}
+        return out
+
+    def reset(self):
+        self.rec = {}
+
+
+TIMER = KernelTimer()
+
+
+def prefill_work(B, Hq, Hkv, Tq, S, d, q_pos0):
+    """Algorithmic flops and HBM bytes of one causal prefill launch."""
+    visible = Tq * q_pos0 + Tq * (Tq + 1) / 2.0            # sum over queries of visible keys
+    flops = 4.0 * d * Hq * B * visible
+    nbytes = 2.0 * (2 * B * Hq * Tq * d + 2 * B * Hkv * S * d) + 4.0 * B * S
+    return flops, nbytes
+
+
 def _stream(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 
@@ -68,6 +113,7 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: fl
         raise ValueError("out must be bf16 [B, Tq, Hq, d] with a contiguous last dim")
     bp, bsb, ep, esb, W = _bias_args(bias, enable, B, Hq, W)
     lib = _lib.load()
+    ev = TIMER.record("cram_prefill", *prefill_work(B, Hq, Hkv, Tq, S, d, q_pos0), q.device) if TIMER.enabled else None
     code = lib.cram_attn_prefill(
         q.data_ptr(), q.stride(0), q.stride(1), q.stride(2),
         k.data_ptr(), k.stride(0), k.stride(1), k.stride(2),
@@ -76,6 +122,8 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: fl
         B, Hq, Hkv, Tq, S, d, int(q_pos0), float(scale),
         bp, bsb, ep, esb, W, _stream(q.device))
     _lib.check(code, "cram_attn_prefill")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(q.device))
     return out
 
 

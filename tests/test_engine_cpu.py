@@ -213,3 +213,22 @@ def test_sweep_flops_accounting():
     f = sweep.sweep_flops(sp, 904, 4)
     ref_fwd = 2 * (6.98e9 + 0.525e9) * 904          # one reference-style full forward
     assert 0.3 * 1025 * ref_fwd < f < 0.6 * 1025 * ref_fwd
+
+
+def test_cpu_baseline_model_matches_engine():
+    """bench.py's CPU baseline runs the same network as the engine (weights copied back into transformers)."""
+    from cram_amd.engine import ModelSpec
+    from oracle import cpu_baseline
+    sp = ModelSpec(2, 256, 4, 2, 128, 512, 1000, 1e-5, False)
+    eng = CrAMEngine.random(sp, torch.device("cpu"), seed=3, std=0.05)
+    model = cpu_baseline.hf_model_from_engine(eng)
+    ids = torch.randint(0, 1000, (1, 77))
+    w = torch.ones((1, 77), dtype=torch.float16)
+    w[:, 10:30] = 0
+    with torch.no_grad():
+        ref = model(input_ids=ids).logits[0, -3:].float()
+    with cpu_ops.patched_ops():
+        got = eng.logits(ids, last=3)[0].float()
+    assert (got - ref).abs().max() < 0.1 and (got - ref).abs().mean() < 0.02
+    r = cpu_baseline.time_ie_units(model, ids, w, torch.tensor([5, 6]), [(0, 1), (1, 2)])
+    assert r["units"] == 2 and r["units_per_s"] > 0 and all(np.isfinite(r["ie"]))
