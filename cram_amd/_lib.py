@@ -44,6 +44,14 @@ SIGNATURES = {
     "cram_answer_logits": (c_int, [
         c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
     ]),
+    "cram_rmsnorm": (c_int, [
+        c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,
+        c_float, c_void_p,
+    ]),
+    "cram_rope_inplace": (c_int, [
+        c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+    ]),
+    "cram_silu_mul": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
 }
 
 _LIB = None

@@ -145,41 +145,34 @@ class CrAMEngine:
                                          / spec.head_dim))
         return CrAMEngine(spec, layers, embed, ones_ish(spec.hidden), lm_head, inv_freq)
 
-    # ------------------------------------------------------------------ elementwise (transformers op order)
+    # ------------------------------------------------------------------ elementwise (fused HIP kernels)
     def rmsnorm(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        xf = x.float()
-        var = xf.pow(2).mean(-1, keepdim=True)
-        return w * (xf * torch.rsqrt(var + self.spec.eps)).to(x.dtype)
+        """LlamaRMSNorm (cram_rmsnorm)."""
+        return ops.rmsnorm(x if x.is_contiguous() else x.contiguous(), w, self.spec.eps)
 
-    def rope_tables(self, pos: torch.Tensor):
-        """pos int64 [..., T] -> cos, sin [..., T, d] in the model dtype (LlamaRotaryEmbedding.forward)."""
-        freqs = pos.float()[..., None] * self.inv_freq
+    def add_rmsnorm(self, delta: torch.Tensor, h: torch.Tensor, w: torch.Tensor):
+        """(h + delta, LlamaRMSNorm(h + delta)) in one pass."""
+        return ops.rmsnorm(delta, w, self.spec.eps, residual=h if h.is_contiguous() else h.contiguous())
+
+    def rope_tables(self, P: int):
+        """bf16 cos, sin [P, d] for positions 0..P-1 (LlamaRotaryEmbedding.forward arithmetic)."""
+        freqs = torch.arange(P, device=self.device, dtype=torch.float32)[:, None] * self.inv_freq[None, :]
         emb = torch.cat((freqs, freqs), dim=-1)
         return (emb.cos() * self.attn_scaling).to(self.dtype), (emb.sin() * self.attn_scaling).to(self.dtype)
 
-    @staticmethod
-    def _rotate_half(x):
-        h = x.shape[-1] // 2
-        return torch.cat((-x[..., h:], x[..., :h]), dim=-1)
-
-    def rope(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
-        """x [..., T, H, d]; cos/sin [..., T, d] (apply_rotary_pos_emb, unsqueeze over heads)."""
-        c, s = cos.unsqueeze(-2), sin.unsqueeze(-2)
-        return (x * c) + (self._rotate_half(x) * s)
-
     def mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
         gu = F.linear(x, lw.wgu)
-        Fi = self.spec.intermediate
-        return F.linear(F.silu(gu[..., :Fi]) * gu[..., Fi:], lw.wd)
+        return F.linear(ops.silu_mul(gu, self.spec.intermediate), lw.wd)
 
-    def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin):
-        """x [..., T, D] -> q [..., T, Hq, d], k, v [..., T, Hkv, d] (roped)."""
+    def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin, pos: Optional[torch.Tensor] = None):
+        """x [B, T, D] -> roped q [B, T, Hq, d], k / v [B, T, Hkv, d]: strided views of one fused buffer."""
         sp = self.spec
         y = F.linear(x, lw.wqkv, lw.bqkv)
+        ops.rope_inplace(y, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=y.shape[-2], pos=pos)
         q = y[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
         k = y[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
         v = y[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
-        return self.rope(q, cos, sin), self.rope(k, cos, sin), v
+        return q, k, v
 
     # ------------------------------------------------------------------ prefill / full forward
     def attention(self, q, k, v, bias: Optional[torch.Tensor] = None, enable: Optional[torch.Tensor] = None,
@@ -200,18 +193,15 @@ class CrAMEngine:
             q = q[:, -out_rows:]
             h = h[:, -out_rows:]
         a = self.attention(q, k, v, bias, enable, W)
-        h = h + F.linear(a.flatten(-2), lw.wo)
-        return h + self.mlp(self.rmsnorm(h, lw.ln2), lw)
-
-    def positions(self, B: int, T: int, start: int = 0) -> torch.Tensor:
-        return torch.arange(start, start + T, device=self.device)[None].expand(B, T)
+        h, x2 = self.add_rmsnorm(F.linear(a.flatten(-2), lw.wo), h, lw.ln2)
+        return h + self.mlp(x2, lw)
 
     @torch.no_grad()
     def forward_hidden(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None, out_rows: Optional[int] = None,
                        kv_out=None, layer_hook=None) -> torch.Tensor:
         """ids [B, T] -> final-norm hidden states [B, T or out_rows, D]."""
         B, T = ids.shape
-        cos, sin = self.rope_tables(self.positions(B, T))
+        cos, sin = self.rope_tables(T)
         h = self.embed[ids]
         L = self.spec.num_layers
         for l in range(L):
@@ -301,6 +291,7 @@ class DecodeSession:
                                dtype=torch.uint8, device=dev) if self.splits > 1 else None)
         self.graph = None
         self.rows = torch.arange(self.B, device=dev)
+        self.cos, self.sin = eng.rope_tables(self.S_max)
 
     def _pick(self, logits: torch.Tensor) -> torch.Tensor:
         if self.bad is not None:
@@ -323,20 +314,19 @@ class DecodeSession:
         self.t.fill_(1)
 
     def _step_body(self):
-        eng, sp = self.eng, self.eng.spec
-        cos, sin = eng.rope_tables(self.pos[:, None])            # [B, 1, d]
+        eng = self.eng
         h = eng.embed[self.tokens][:, None]                      # [B, 1, D]
         self.seq_lens.add_(1)
         for l, lw in enumerate(eng.layers):
             x = eng.rmsnorm(h, lw.ln1)
-            q, k, v = eng.qkv(x, lw, cos, sin)
+            q, k, v = eng.qkv(x, lw, self.cos, self.sin, pos=self.pos)
             self.k_cache[l, self.rows, :, self.pos] = k[:, 0]
             self.v_cache[l, self.rows, :, self.pos] = v[:, 0]
             a = ops.attn_decode(q[:, 0], self.k_cache[l], self.v_cache[l], scale=eng.scale, seq_lens=self.seq_lens,
                                 bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
                                 workspace=self.ws)
-            h = h + F.linear(a.flatten(-2)[:, None], lw.wo)
-            h = h + eng.mlp(eng.rmsnorm(h, lw.ln2), lw)
+            h, x2 = eng.add_rmsnorm(F.linear(a.flatten(-2)[:, None], lw.wo), h, lw.ln2)
+            h = h + eng.mlp(x2, lw)
         hn = eng.rmsnorm(h[:, 0], eng.norm)
         nxt = self._pick(F.linear(hn, eng.lm_head))
         self.tokens.copy_(nxt)

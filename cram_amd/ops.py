@@ -187,3 +187,63 @@ def answer_logits(hidden: torch.Tensor, w_lm: torch.Tensor, ids: torch.Tensor, *
                                   _stream(hidden.device))
     _lib.check(code, "cram_answer_logits")
     return out
+
+
+def _rows2d(t: torch.Tensor, name: str) -> torch.Tensor:
+    """View [..., C] with contiguous last dim as rows (returns the 2-D view; raises if not row-uniform)."""
+    if t.stride(-1) != 1:
+        raise ValueError(f"{name} must have a contiguous last dimension")
+    if t.dim() == 2:
+        return t
+    try:
+        return t.view(-1, t.shape[-1])
+    except RuntimeError:
+        raise ValueError(f"{name} rows are not uniformly strided") from None
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+            h_out: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+    """LlamaRMSNorm(x [+ residual]).  Returns y, or (h, y) when residual is given (h = x + residual)."""
+    _check_bf16("w", w, 1)
+    x2 = _rows2d(x, "x")
+    rows, D = x2.shape
+    if out is None:
+        out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+    y2 = _rows2d(out, "out")
+    r2 = h2 = None
+    if residual is not None:
+        r2 = _rows2d(residual, "residual")
+        if h_out is None:
+            h_out = torch.empty(x.shape, dtype=x.dtype, device=x.device)
+        h2 = _rows2d(h_out, "h_out")
+    code = _lib.load().cram_rmsnorm(x2.data_ptr(), x2.stride(0), _ptr(r2), r2.stride(0) if r2 is not None else 0,
+                                    _ptr(h2), h2.stride(0) if h2 is not None else 0, w.data_ptr(), y2.data_ptr(),
+                                    y2.stride(0), rows, D, float(eps), _stream(x.device))
+    _lib.check(code, "cram_rmsnorm")
+    return (h_out, out) if residual is not None else out
+
+
+def rope_inplace(qkv: torch.Tensor, heads: int, head_dim: int, cos: torch.Tensor, sin: torch.Tensor, T: int,
+                 pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Rotate the first `heads` heads of every row of the fused QKV buffer in place (apply_rotary_pos_emb)."""
+    y2 = _rows2d(qkv, "qkv")
+    if cos.dtype != torch.bfloat16 or cos.shape != sin.shape or cos.stride(-1) != 1:
+        raise ValueError("cos/sin must be bf16 [P, d] tables")
+    if pos is not None and (pos.dtype != torch.int64 or pos.numel() != y2.shape[0]):
+        raise ValueError("pos must be int64 with one entry per row")
+    code = _lib.load().cram_rope_inplace(y2.data_ptr(), y2.stride(0), y2.shape[0], int(T), int(heads), int(head_dim),
+                                         cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), _stream(qkv.device))
+    _lib.check(code, "cram_rope_inplace")
+    return qkv
+
+
+def silu_mul(gu: torch.Tensor, F: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16(silu(gu[..., :F])) * gu[..., F:2F] (LlamaMLP activation)."""
+    g2 = _rows2d(gu, "gu")
+    if out is None:
+        out = torch.empty(gu.shape[:-1] + (F,), dtype=gu.dtype, device=gu.device)
+    y2 = _rows2d(out, "out")
+    code = _lib.load().cram_silu_mul(g2.data_ptr(), g2.stride(0), y2.data_ptr(), y2.stride(0), g2.shape[0], int(F),
+                                     _stream(gu.device))
+    _lib.check(code, "cram_silu_mul")
+    return out

@@ -52,7 +52,7 @@ def baseline(eng: CrAMEngine, ids: torch.Tensor, n_ans: int, keep: bool = True):
     """Un-hooked forward; returns (final hidden of the last n rows [n, D], QuestionCache)."""
     sp = eng.spec
     T = ids.shape[-1]
-    cos, sin = eng.rope_tables(eng.positions(1, T))
+    cos, sin = eng.rope_tables(T)
     h = eng.embed[ids.view(1, T)]
     qc = QuestionCache()
     L = sp.num_layers
@@ -70,8 +70,8 @@ def baseline(eng: CrAMEngine, ids: torch.Tensor, n_ans: int, keep: bool = True):
         if l == L - 1:
             a = a[:, -n_ans:]
             h = h[:, -n_ans:]
-        h = h + F.linear(a.flatten(-2), lw.wo)
-        h = h + eng.mlp(eng.rmsnorm(h, lw.ln2), lw)
+        h, x2 = eng.add_rmsnorm(F.linear(a.flatten(-2), lw.wo), h, lw.ln2)
+        h = h + eng.mlp(x2, lw)
     return eng.rmsnorm(h, eng.norm)[0], qc
 
 
@@ -97,10 +97,11 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     idx = torch.arange(Hv - 1, device=eng.device)
     x[idx, :, heads] = a_bias[0].permute(1, 0, 2)[heads]                # variant i <- biased head heads[i]
     lw = eng.layers[l]
-    h = qc.h_in[l][:, -rows:] + F.linear(x.flatten(-2), lw.wo)         # [Hv, rows, D]
-    h = h + eng.mlp(eng.rmsnorm(h, lw.ln2), lw)
+    h_in = qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden)
+    h, x2 = eng.add_rmsnorm(F.linear(x.flatten(-2), lw.wo), h_in, lw.ln2)   # [Hv, rows, D]
+    h = h + eng.mlp(x2, lw)
     if not last:
-        cos, sin = eng.rope_tables(eng.positions(Hv, T))
+        cos, sin = eng.rope_tables(T)
         for l2 in range(l + 1, L):
             h = eng.layer(h, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None)
     return eng.rmsnorm(h, eng.norm)                                   # [Hv, n, D]

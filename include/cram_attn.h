@@ -99,6 +99,25 @@ int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64
                        const int32_t* ids, int n, int D, int round_bf16, float* out,
                        cram_stream_t stream);
 
+/*
+ * Fused elementwise kernels of the engine (cram_fused.hip), bf16, rows of 16-byte aligned vectors.
+ * They keep transformers' rounding points (LlamaRMSNorm, apply_rotary_pos_emb, LlamaMLP), i.e. the
+ * arithmetic the reference's hooked model runs between its GEMMs (re_weighting.py:127 -> generate,
+ * :159/:169 -> model forward).
+ *
+ * cram_rmsnorm       y = bf16(w * bf16(h * rsqrt(mean(h^2) + eps))) per row; if residual != NULL then
+ *                    h = bf16(x + residual) is also written to h_out, else h = x.
+ * cram_rope_inplace  rotates the first `heads` heads (q then k) of every row of a fused QKV buffer in
+ *                    place; row r uses position pos[r] (int64) or r % T when pos == NULL; cos/sin are
+ *                    bf16 [P][d] tables (row stride tab_rs).
+ * cram_silu_mul      y[r, :F] = bf16(bf16(silu(gu[r, :F])) * gu[r, F:2F])
+ */
+int cram_rmsnorm(const void* x, int64_t x_rs, const void* residual, int64_t r_rs, void* h_out, int64_t h_rs,
+                 const void* w, void* y, int64_t y_rs, int rows, int D, float eps, cram_stream_t stream);
+int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads, int d, const void* cos_t,
+                      const void* sin_t, int64_t tab_rs, const int64_t* pos, cram_stream_t stream);
+int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, cram_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,13 +66,40 @@ def decode_workspace_bytes(B, Hq, d, num_splits):
     return 0
 
 
+def rmsnorm(x, w, eps, residual=None, h_out=None, out=None):
+    h = x if residual is None else (residual + x)
+    hf = h.float()
+    y = w * (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype)
+    return (h, y) if residual is not None else y
+
+
+def rope_inplace(qkv, heads, head_dim, cos, sin, T, pos=None):
+    shp = qkv.shape
+    y = qkv.reshape(-1, shp[-1])
+    rows = y.shape[0]
+    p = pos.reshape(-1) if pos is not None else torch.arange(rows) % T
+    c, s_ = cos[p][:, None, :], sin[p][:, None, :]
+    x = y[:, :heads * head_dim].view(rows, heads, head_dim)
+    h = head_dim // 2
+    rot = torch.cat((-x[..., h:], x[..., :h]), dim=-1)
+    y[:, :heads * head_dim] = ((x * c) + (rot * s_)).reshape(rows, -1)
+    return qkv
+
+
+def silu_mul(gu, F, out=None):
+    return torch.nn.functional.silu(gu[..., :F]) * gu[..., F:]
+
+
 @contextlib.contextmanager
 def patched_ops():
     """Route cram_amd.ops through the CPU stand-ins for the duration of a CPU test."""
     from cram_amd import ops
-    saved = {n: getattr(ops, n) for n in ("attn_prefill", "attn_decode", "answer_logits", "decode_workspace_bytes")}
-    ops.attn_prefill, ops.attn_decode, ops.answer_logits = attn_prefill, attn_decode, answer_logits
-    ops.decode_workspace_bytes = decode_workspace_bytes
+    names = ("attn_prefill", "attn_decode", "answer_logits", "decode_workspace_bytes", "rmsnorm", "rope_inplace",
+             "silu_mul")
+    saved = {n: getattr(ops, n) for n in names}
+    g = globals()
+    for n in names:
+        setattr(ops, n, g[n])
     try:
         yield
     finally:

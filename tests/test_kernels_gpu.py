@@ -136,3 +136,78 @@ def test_rejects_bad_alignment(gpu_device):
     q = torch.randn(1, 2, 4, 100, device=dev).to(torch.bfloat16)   # d = 100 unsupported
     with pytest.raises(RuntimeError):
         ops.attn_prefill(q, q[:, :1], q[:, :1], scale=0.1)
+
+
+# ----------------------------------------------------------------------------------------------
+# fused elementwise kernels vs transformers' op sequences (LlamaRMSNorm, apply_rotary_pos_emb, LlamaMLP)
+# ----------------------------------------------------------------------------------------------
+def _ulp_diff(a, b):
+    """bf16 ulp distance per element."""
+    ai = a.view(torch.int16).to(torch.int32)
+    bi = b.view(torch.int16).to(torch.int32)
+    ai = torch.where(ai < 0, -(ai & 0x7FFF), ai)
+    bi = torch.where(bi < 0, -(bi & 0x7FFF), bi)
+    return (ai - bi).abs()
+
+
+@pytest.mark.parametrize("D", [256, 3584, 4096])
+@pytest.mark.parametrize("with_residual", [False, True])
+def test_rmsnorm_matches_transformers(gpu_device, D, with_residual):
+    from cram_amd import ops
+    dev = gpu_device
+    g = torch.Generator(device=dev).manual_seed(D)
+    x = torch.randn(3, 77, D, device=dev, generator=g).to(torch.bfloat16)
+    r = torch.randn(3, 77, D, device=dev, generator=g).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(D, device=dev, generator=g)).to(torch.bfloat16)
+    h = (r + x) if with_residual else x
+    hf = h.float()
+    ref = w * (hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)).to(torch.bfloat16)
+    if with_residual:
+        h_got, got = ops.rmsnorm(x, w, 1e-5, residual=r)
+        assert torch.equal(h_got, h)
+    else:
+        got = ops.rmsnorm(x, w, 1e-5)
+    ud = _ulp_diff(got, ref)
+    assert ud.max() <= 1 and (ud == 0).float().mean() > 0.995, (ud.max().item(), (ud == 0).float().mean().item())
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (28, 4), (4, 2)])
+def test_rope_bit_exact(gpu_device, Hq, Hkv):
+    from cram_amd import ops
+    from cram_amd.engine import CrAMEngine, ModelSpec
+    dev = gpu_device
+    d = 128
+    sp = ModelSpec(1, Hq * d, Hq, Hkv, d, 256, 100, 1e-5, False)
+    eng = CrAMEngine.random(sp, dev, seed=1)
+    B, T = 2, 131
+    N = (Hq + 2 * Hkv) * d
+    y = torch.randn(B, T, N, device=dev).to(torch.bfloat16)
+    cos, sin = eng.rope_tables(T)
+    # transformers: q_embed = (q * cos) + (rotate_half(q) * sin), heads unsqueezed
+    x = y[..., :(Hq + Hkv) * d].unflatten(-1, (Hq + Hkv, d))
+    c, s = cos[None, :, None, :], sin[None, :, None, :]
+    rot = torch.cat((-x[..., d // 2:], x[..., :d // 2]), dim=-1)
+    ref = (x * c) + (rot * s)
+    v_before = y[..., (Hq + Hkv) * d:].clone()
+    ops.rope_inplace(y, Hq + Hkv, d, cos, sin, T)
+    assert torch.equal(y[..., :(Hq + Hkv) * d].unflatten(-1, (Hq + Hkv, d)), ref)
+    assert torch.equal(y[..., (Hq + Hkv) * d:], v_before)
+    # per-row positions (decode)
+    y2 = torch.randn(5, 1, N, device=dev).to(torch.bfloat16)
+    pos = torch.tensor([0, 7, 130, 64, 3], device=dev)
+    x2 = y2[:, 0, :(Hq + Hkv) * d].unflatten(-1, (Hq + Hkv, d))
+    rot2 = torch.cat((-x2[..., d // 2:], x2[..., :d // 2]), dim=-1)
+    ref2 = (x2 * cos[pos][:, None]) + (rot2 * sin[pos][:, None])
+    ops.rope_inplace(y2, Hq + Hkv, d, cos, sin, 1, pos=pos)
+    assert torch.equal(y2[:, 0, :(Hq + Hkv) * d].unflatten(-1, (Hq + Hkv, d)), ref2)
+
+
+@pytest.mark.parametrize("F", [512, 14336, 18944])
+def test_silu_mul_matches_transformers(gpu_device, F):
+    from cram_amd import ops
+    dev = gpu_device
+    gu = (2 * torch.randn(3, 50, 2 * F, device=dev)).to(torch.bfloat16)
+    ref = torch.nn.functional.silu(gu[..., :F]) * gu[..., F:]
+    got = ops.silu_mul(gu, F)
+    ud = _ulp_diff(got, ref)
+    assert ud.max() <= 1 and (ud == 0).float().mean() > 0.995, (ud.max().item(), (ud == 0).float().mean().item())
