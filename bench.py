@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-units", type=int, default=2)
+    ap.add_argument("--blas", default="hipblaslt", choices=["hipblas", "hipblaslt"])
     args = ap.parse_args()
 
     import torch
@@ -62,6 +63,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
 
+    from cram_amd.engine import configure_blas
+    configure_blas(args.blas)
     spec = ModelSpec.llama3_8b() if args.model == "llama3-8b" else ModelSpec.qwen2_7b()
     t0 = time.time()
     eng = CrAMEngine.random(spec, dev, seed=1234, rope_theta=500000.0 if args.model == "llama3-8b" else 1e6)

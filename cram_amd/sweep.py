@@ -32,8 +32,9 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
+from . import ops
 from .bias import CredibilityBias
-from .engine import CrAMEngine
+from .engine import CrAMEngine, padded_rows
 
 
 class QuestionCache:
@@ -93,18 +94,23 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
         q = q[:, -n_ans:]
     a_bias = eng.attention(q, k, v, bias, enable, W)                   # [1, rows, Hq, d] every head biased
     a_base = qc.a[l][:, -rows:]
-    x = a_base.expand(Hv, rows, H, sp.head_dim).clone()                # [Hv, rows, Hq, d]
+    M = Hv * rows
+    Mp = M if last else padded_rows(M)                                  # GEMM rows aligned to the macro tile
+    abuf = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=eng.device)
+    x = abuf[:M].view(Hv, rows, H, sp.head_dim)
+    x.copy_(a_base.expand(Hv, rows, H, sp.head_dim))                    # [Hv, rows, Hq, d]
     idx = torch.arange(Hv - 1, device=eng.device)
     x[idx, :, heads] = a_bias[0].permute(1, 0, 2)[heads]                # variant i <- biased head heads[i]
     lw = eng.layers[l]
-    h_in = qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden)
-    h, x2 = eng.add_rmsnorm(F.linear(x.flatten(-2), lw.wo), h_in, lw.ln2)   # [Hv, rows, D]
+    hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
+    hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
+    h, x2 = ops.rmsnorm(F.linear(abuf, lw.wo), lw.ln2, sp.eps, residual=hin)   # [Mp, D]
     h = h + eng.mlp(x2, lw)
     if not last:
         cos, sin = eng.rope_tables(T)
         for l2 in range(l + 1, L):
-            h = eng.layer(h, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None)
-    return eng.rmsnorm(h, eng.norm)                                   # [Hv, n, D]
+            h = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None)
+    return eng.rmsnorm(h[:Hv * n_ans], eng.norm).view(Hv, n_ans, sp.hidden)   # [Hv, n, D]
 
 
 @torch.no_grad()

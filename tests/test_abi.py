@@ -1,0 +1,64 @@
+"""The C-ABI library loads (no GPU needed) and exports exactly what include/cram_attn.h declares."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(REPO, "include", "cram_attn.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cram_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for n in ("cram_attn_prefill", "cram_attn_decode", "cram_attn_decode_workspace_size", "cram_answer_logits",
+              "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_silu_mul"):
+        assert n in names
+
+
+def test_library_builds_loads_and_exports_every_symbol():
+    from cram_amd import build, _lib
+    build.build()
+    lib = ctypes.CDLL(str(build.LIB_PATH))
+    for n in _declared():
+        assert hasattr(lib, n), n
+    assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
+    L = _lib.load()
+    assert L.cram_abi_version() == 1
+    assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
+    assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
+    assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0
+
+
+def test_argument_validation_without_gpu():
+    """Bad arguments are rejected on the host before any launch (no device needed)."""
+    from cram_amd import _lib
+    L = _lib.load()
+    # null pointers
+    assert L.cram_attn_prefill(None, 0, 0, 0, None, 0, 0, 0, None, 0, 0, 0, None, 0, 0, 0,
+                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, None) == -1
+    # unsupported head dim (checked before alignment / launch)
+    fake = 1 << 20
+    assert L.cram_attn_prefill(fake, 0, 0, 0, fake, 0, 0, 0, fake, 0, 0, 0, fake, 0, 0, 0,
+                               1, 1, 1, 1, 1, 96, 0, 1.0, None, 0, None, 0, 0, None) == -2
+    # misaligned stride
+    assert L.cram_attn_prefill(fake, 8, 8, 12, fake, 0, 0, 8, fake, 0, 0, 8, fake, 0, 0, 8,
+                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, None) == -3
+    # split decode without workspace
+    assert L.cram_attn_decode(fake, 0, 0, fake, 0, 0, 8, fake, 0, 0, 8, fake, 0, 0,
+                              1, 1, 1, 4, None, 128, 1.0, None, 0, None, 0, 0, 4, None, 0, None) == -5
+    assert L.cram_rmsnorm(None, 0, None, 0, None, 0, None, None, 0, 1, 8, 1e-5, None) == -1
+    assert L.cram_silu_mul(fake, 8, fake, 8, 1, 12, None) == -3
+
+
+def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):
+    from cram_amd import _lib
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", tmp_path / "missing.so")
+    with pytest.raises(_lib.CrAMLibraryError):
+        _lib.load()
