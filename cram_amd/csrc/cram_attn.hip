@@ -31,6 +31,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -127,39 +128,49 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   const int wave_qpos_min = p.q_pos0 + q_row0;
   const int wave_qpos_max = p.q_pos0 + min(q_row0 + 31, p.Tq - 1);
 
-  uint4 kst[C::CPT], vst[C::CPT];
+  // K/V/bias staging through buffer descriptors: per-thread byte offsets are loop invariant, the
+  // per-tile base and the valid extent live in scalar registers, and the descriptor's range check
+  // returns zeros past key S (no per-load VALU address math, no bounds compares).
+  uint32_t koff[C::CPT], voff[C::CPT], ldsk[C::CPT], ldsv[C::CPT];
+#pragma unroll
+  for (int i = 0; i < C::CPT; ++i) {
+    const int c = tid + 256 * i;
+    const int row = c / C::CPR, col = c % C::CPR;
+    koff[i] = (uint32_t)((row * p.k_st + col * 8) * 2);
+    voff[i] = (uint32_t)((row * p.v_st + col * 8) * 2);
+    ldsk[i] = row * C::KSTR + col * 16;
+    ldsv[i] = C::K_BYTES + row * C::VSTR + col * 16;
+  }
+  u32x4 kst[C::CPT], vst[C::CPT];
   float bst = 0.f;
 
   auto gload = [&](int t) {
     const int key0 = t * C::BK;
+    const int rows_left = p.S - key0;   // > 0 for every tile of the loop
+    const auto ksrd = __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (int64_t)key0 * p.k_st), (short)0,
+                                                        (int)((rows_left - 1) * p.k_st * 2 + D * 2), 0x00020000);
+    const auto vsrd = __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (int64_t)key0 * p.v_st), (short)0,
+                                                        (int)((rows_left - 1) * p.v_st * 2 + D * 2), 0x00020000);
 #pragma unroll
     for (int i = 0; i < C::CPT; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c / C::CPR, col = c % C::CPR;
-      const int key = key0 + row;
-      if (key < p.S) {
-        kst[i] = *reinterpret_cast<const uint4*>(kbase + key * p.k_st + col * 8);
-        vst[i] = *reinterpret_cast<const uint4*>(vbase + key * p.v_st + col * 8);
-      } else {
-        kst[i] = make_uint4(0, 0, 0, 0);
-        vst[i] = make_uint4(0, 0, 0, 0);
-      }
+      kst[i] = __builtin_amdgcn_raw_buffer_load_b128(ksrd, (int)koff[i], 0, 0);
+      vst[i] = __builtin_amdgcn_raw_buffer_load_b128(vsrd, (int)voff[i], 0, 0);
     }
-    if (tid < C::BK) {
-      const int key = key0 + tid;
-      bst = (en && key < p.W) ? brow[key] * kLog2e : 0.f;
+    if (en && tid < C::BK) {
+      const int wl = p.W - key0;
+      const auto bsrd = __builtin_amdgcn_make_buffer_rsrc((void*)(brow + key0), (short)0, wl > 0 ? wl * 4 : 0,
+                                                          0x00020000);
+      bst = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, tid * 4, 0, 0)) * kLog2e;
     }
   };
   auto swrite = [&](int buf) {
     char* base = smem + buf * C::STAGE;
 #pragma unroll
     for (int i = 0; i < C::CPT; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c / C::CPR, col = c % C::CPR;
-      *reinterpret_cast<uint4*>(base + row * C::KSTR + col * 16) = kst[i];
-      *reinterpret_cast<uint4*>(base + C::K_BYTES + row * C::VSTR + col * 16) = vst[i];
+      *reinterpret_cast<u32x4*>(base + ldsk[i]) = kst[i];
+      *reinterpret_cast<u32x4*>(base + ldsv[i]) = vst[i];
     }
-    if (tid < C::BK) reinterpret_cast<float*>(base + C::K_BYTES + C::V_BYTES)[tid] = bst;
+    if (en && tid < C::BK) reinterpret_cast<float*>(base + C::K_BYTES + C::V_BYTES)[tid] = bst;
   };
 
   float m = kNegInf, l = 0.f;
@@ -186,14 +197,13 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
     if (wave_live && key0 <= wave_qpos_max) {
       const char* base = smem + (t & 1) * C::STAGE;
       f32x16 sacc[2];
+      const f32x16 zero16 = {};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) sacc[kb][e] = 0.f;
-#pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
-          sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], sacc[kb], 0, 0, 0);
+          sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], ks == 0 ? zero16 : sacc[kb], 0, 0, 0);
         }
       }
       // scores (log2 units): scale, credibility bias, causal / length mask
@@ -233,10 +243,14 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       rs = half_sum(rs);
       l = l * alpha + rs;
       m = mnew;
+      // the running max rarely moves after the first tiles: skip the O rescale when alpha == 1 on
+      // every lane (exact; a wave-uniform branch)
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
-      for (int db = 0; db < D / 32; ++db)
+        for (int db = 0; db < D / 32; ++db)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) oacc[db][e] *= alpha;
+          for (int e = 0; e < 16; ++e) oacc[db][e] *= alpha;
+      }
 
       // O^T[dv][q] += V^T[dv][key] . P^T[key][q]
       const char* vimg = base + C::K_BYTES;
@@ -555,6 +569,9 @@ int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, c
       !m8(v_st) || !m8(o_sb) || !m8(o_sh) || !m8(o_st))
     return CRAM_ERR_ALIGNMENT;
   if (bias && W < 0) return CRAM_ERR_INVALID_ARG;
+  // buffer-descriptor extents are 32-bit byte counts
+  if ((int64_t)S * (k_st > v_st ? k_st : v_st) * 2 + 2 * d >= (1ll << 31) || (int64_t)W * 4 >= (1ll << 31))
+    return CRAM_ERR_UNSUPPORTED;
   PrefillParams p;
   p.q = (const __bf16*)q; p.q_sb = q_sb; p.q_sh = q_sh; p.q_st = q_st;
   p.k = (const __bf16*)k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
