@@ -57,6 +57,22 @@ def snake_layers(num_layers: int, world: int) -> List[List[int]]:
     return bins
 
 
+def _comm_device(t: torch.Tensor, group=None) -> torch.device:
+    """Where a collective on `t` must run: gloo only moves host tensors (rehearsal runs on one GPU)."""
+    if dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return t.device
+
+
+def all_reduce_host(t: torch.Tensor, op: str = "sum", group=None) -> torch.Tensor:
+    """All-reduce a small tensor with the process group's backend; returns it on t's device."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    x = t.to(_comm_device(t, group))
+    dist.all_reduce(x, op={"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op], group=group)
+    return x.to(t.device)
+
+
 def gather_rows(local: torch.Tensor, local_ids: torch.Tensor, n_total: int, group=None) -> torch.Tensor:
     """All-gather per-rank rows (ragged counts) into a dense [n_total, ...] tensor on every rank.
 
@@ -67,7 +83,9 @@ def gather_rows(local: torch.Tensor, local_ids: torch.Tensor, n_total: int, grou
         out = torch.zeros((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         out[local_ids.to(local.device)] = local
         return out
-    dev = local.device
+    home = local.device
+    dev = _comm_device(local, group)
+    local = local.to(dev)
     kmax_t = torch.tensor([local.shape[0]], device=dev, dtype=torch.int64)
     dist.all_reduce(kmax_t, op=dist.ReduceOp.MAX, group=group)
     kmax = int(kmax_t.item())
@@ -82,7 +100,7 @@ def gather_rows(local: torch.Tensor, local_ids: torch.Tensor, n_total: int, grou
     ids = allb[keep, 0].long()
     out = torch.zeros((n_total, row), dtype=torch.float64, device=dev)
     out[ids] = allb[keep, 1:]
-    return out.reshape((n_total,) + tuple(local.shape[1:])).to(local.dtype)
+    return out.reshape((n_total,) + tuple(local.shape[1:])).to(device=home, dtype=local.dtype)
 
 
 def sweep_questions(fn, n_questions: int, costs: Sequence[float], row_shape: Tuple[int, ...], device,
