@@ -30,6 +30,11 @@ SIGNATURES = {
         c_void_p, c_int64, c_void_p, c_int64, c_int,
         c_void_p,
     ]),
+    "cram_attn_prefill_varlen": (c_int, [
+        c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
+        c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p,
+    ]),
     "cram_attn_decode_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cram_attn_decode": (c_int, [
         c_void_p, c_int64, c_int64,

@@ -62,6 +62,7 @@ struct PrefillParams {
   int B, Hq, Hkv, Tq, S, W, q_pos0;
   float scale_log2;  // softmax scale * log2(e)
   int nqb, nblocks;
+  const int32_t* cu;  // varlen: [B+1] token offsets of packed sequences (q/k/v/o batch strides unused)
 };
 
 template <int D>
@@ -97,15 +98,24 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   const int G = p.Hq / p.Hkv;
   const int hkv = hq / G;
 
+  // per-sequence extent: uniform batch, or packed varlen sequences (cu_seqlens)
+  int Tq = p.Tq, S = p.S, q_pos0 = p.q_pos0;
+  int64_t tok0 = 0;
+  if (p.cu) {
+    tok0 = p.cu[b];
+    Tq = S = p.cu[b + 1] - (int)tok0;
+    q_pos0 = 0;
+    if (qblk * C::BQ >= Tq) return;   // whole workgroup exits before any barrier
+  }
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, hh = lane >> 5;
   const int q_row0 = qblk * C::BQ + wave * 32;
   const int qrow = q_row0 + r;
-  const int qpos = p.q_pos0 + qrow;
+  const int qpos = q_pos0 + qrow;
 
-  const __bf16* qb = p.q + b * p.q_sb + hq * p.q_sh;
-  const __bf16* kbase = p.k + b * p.k_sb + hkv * p.k_sh;
-  const __bf16* vbase = p.v + b * p.v_sb + hkv * p.v_sh;
+  const __bf16* qb = p.q + b * p.q_sb + tok0 * p.q_st + hq * p.q_sh;
+  const __bf16* kbase = p.k + b * p.k_sb + tok0 * p.k_st + hkv * p.k_sh;
+  const __bf16* vbase = p.v + b * p.v_sb + tok0 * p.v_st + hkv * p.v_sh;
   const bool en = (p.bias != nullptr) && (p.enable != nullptr) && p.enable[b * p.en_sb + hq] != 0;
   const float* brow = en ? p.bias + b * p.bias_sb : nullptr;
 
@@ -113,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   bf16x8 qf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
-    if (qrow < p.Tq) {
+    if (qrow < Tq) {
       qf[ks] = *reinterpret_cast<const bf16x8*>(qb + qrow * p.q_st + 16 * ks + 8 * hh);
     } else {
 #pragma unroll
@@ -121,12 +131,12 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
     }
   }
 
-  const int blk_last_q = min(qblk * C::BQ + C::BQ, p.Tq) - 1;
-  const int kv_end = min(p.S, p.q_pos0 + blk_last_q + 1);
+  const int blk_last_q = min(qblk * C::BQ + C::BQ, Tq) - 1;
+  const int kv_end = min(S, q_pos0 + blk_last_q + 1);
   const int nt = (kv_end + C::BK - 1) / C::BK;
-  const bool wave_live = q_row0 < p.Tq;
-  const int wave_qpos_min = p.q_pos0 + q_row0;
-  const int wave_qpos_max = p.q_pos0 + min(q_row0 + 31, p.Tq - 1);
+  const bool wave_live = q_row0 < Tq;
+  const int wave_qpos_min = q_pos0 + q_row0;
+  const int wave_qpos_max = q_pos0 + min(q_row0 + 31, Tq - 1);
 
   // K/V/bias staging through buffer descriptors: per-thread byte offsets are loop invariant, the
   // per-tile base and the valid extent live in scalar registers, and the descriptor's range check
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
 
   auto gload = [&](int t) {
     const int key0 = t * C::BK;
-    const int rows_left = p.S - key0;   // > 0 for every tile of the loop
+    const int rows_left = S - key0;   // > 0 for every tile of the loop
     const auto ksrd = __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (int64_t)key0 * p.k_st), (short)0,
                                                         (int)((rows_left - 1) * p.k_st * 2 + D * 2), 0x00020000);
     const auto vsrd = __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (int64_t)key0 * p.v_st), (short)0,
@@ -208,8 +218,8 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       }
       // scores (log2 units): scale, credibility bias, causal / length mask
       const float* bl = reinterpret_cast<const float*>(base + C::K_BYTES + C::V_BYTES);
-      const bool need_mask = (key0 + C::BK - 1 > wave_qpos_min) || (key0 + C::BK > p.S);
-      const int lim = min(qpos, p.S - 1) - key0;
+      const bool need_mask = (key0 + C::BK - 1 > wave_qpos_min) || (key0 + C::BK > S);
+      const int lim = min(qpos, S - 1) - key0;
       float mx = kNegInf;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -280,9 +290,9 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
     __syncthreads();
   }
 
-  if (qrow < p.Tq) {
+  if (qrow < Tq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    __bf16* ob = p.o + b * p.o_sb + hq * p.o_sh + qrow * p.o_st;
+    __bf16* ob = p.o + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh + qrow * p.o_st;
 #pragma unroll
     for (int db = 0; db < D / 32; ++db)
 #pragma unroll
@@ -581,6 +591,34 @@ int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, c
   p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = Tq; p.S = S; p.W = bias ? W : 0; p.q_pos0 = q_pos0;
   p.scale_log2 = scale * kLog2e;
+  p.cu = nullptr;
+  return d == 128 ? launch_prefill<128>(p, (hipStream_t)stream) : launch_prefill<64>(p, (hipStream_t)stream);
+}
+
+int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sh, int64_t k_st,
+                             const void* v, int64_t v_sh, int64_t v_st, void* o, int64_t o_sh, int64_t o_st,
+                             const int32_t* cu_seqlens, int B, int max_len, int Hq, int Hkv, int d, float scale,
+                             const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                             cram_stream_t stream) {
+  if (!q || !k || !v || !o || !cu_seqlens) return CRAM_ERR_INVALID_ARG;
+  if (B <= 0 || Hq <= 0 || Hkv <= 0 || max_len <= 0 || Hq % Hkv != 0) return CRAM_ERR_INVALID_ARG;
+  if (d != 64 && d != 128) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return CRAM_ERR_ALIGNMENT;
+  if (!m8(q_sh) || !m8(q_st) || !m8(k_sh) || !m8(k_st) || !m8(v_sh) || !m8(v_st) || !m8(o_sh) || !m8(o_st))
+    return CRAM_ERR_ALIGNMENT;
+  if (bias && W < 0) return CRAM_ERR_INVALID_ARG;
+  if ((int64_t)max_len * (k_st > v_st ? k_st : v_st) * 2 + 2 * d >= (1ll << 31) || (int64_t)W * 4 >= (1ll << 31))
+    return CRAM_ERR_UNSUPPORTED;
+  PrefillParams p;
+  p.q = (const __bf16*)q; p.q_sb = 0; p.q_sh = q_sh; p.q_st = q_st;
+  p.k = (const __bf16*)k; p.k_sb = 0; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = (const __bf16*)v; p.v_sb = 0; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = (__bf16*)o; p.o_sb = 0; p.o_sh = o_sh; p.o_st = o_st;
+  p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
+  p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
+  p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = max_len; p.S = max_len; p.W = bias ? W : 0; p.q_pos0 = 0;
+  p.scale_log2 = scale * kLog2e;
+  p.cu = cu_seqlens;
   return d == 128 ? launch_prefill<128>(p, (hipStream_t)stream) : launch_prefill<64>(p, (hipStream_t)stream);
 }
 

@@ -342,6 +342,47 @@ class DecodeSession:
         return torch.argmax(logits, dim=-1)
 
     def prefill(self):
+        """All prompts in ONE packed pass (GEMM M = sum of prompt lengths, rounded to 256 rows);
+        attention per sequence through cram_attn_prefill_varlen; K/V scattered into the cache."""
+        eng, sp = self.eng, self.eng.spec
+        dev = eng.device
+        lens = self.lens
+        total = sum(lens)
+        Mp = padded_rows(total)
+        offs = [0]
+        for n in lens:
+            offs.append(offs[-1] + n)
+        cu = torch.tensor(offs, dtype=torch.int32, device=dev)
+        pos = torch.cat([torch.arange(n, device=dev) for n in lens])
+        bidx = torch.cat([torch.full((n,), b, device=dev, dtype=torch.long) for b, n in enumerate(lens)])
+        h = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=dev)
+        h[:total] = eng.embed[torch.cat(self.prompts)]
+        if Mp > total:
+            h[total:].zero_()
+        for l, lw in enumerate(eng.layers):
+            x = ops.rmsnorm(h, lw.ln1, sp.eps)
+            y = F.linear(x, lw.wqkv, lw.bqkv)
+            yr = y[:total]
+            ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, self.cos, self.sin, T=1, pos=pos)
+            q = yr[:, :sp.q_size].view(total, sp.num_heads, sp.head_dim)
+            k = yr[:, sp.q_size:sp.q_size + sp.kv_size].view(total, sp.num_kv_heads, sp.head_dim)
+            v = yr[:, sp.q_size + sp.kv_size:].view(total, sp.num_kv_heads, sp.head_dim)
+            self.k_cache[l, bidx, :, pos] = k
+            self.v_cache[l, bidx, :, pos] = v
+            a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
+            if Mp > total:
+                a[total:].zero_()
+            ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=self.cb.bias,
+                                    enable=self.cb.enable[l], W=self.cb.W,
+                                    out=a[:total].view(total, sp.num_heads, sp.head_dim))
+            h, x2 = ops.rmsnorm(F.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
+            h = h + eng.mlp(x2, lw)
+        hn = eng.rmsnorm(h[cu[1:].long() - 1], eng.norm)
+        self.tokens.copy_(self._pick(F.linear(hn, eng.lm_head)))
+        self.out[:, 0] = self.tokens
+        self.t.fill_(1)
+
+    def prefill_one_by_one(self):
         eng = self.eng
         for b, ids in enumerate(self.prompts):
             T = ids.numel()

@@ -127,6 +127,34 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: fl
     return out
 
 
+def attn_prefill_varlen(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor, max_len: int, *,
+                        scale: float, bias: Optional[torch.Tensor] = None, enable: Optional[torch.Tensor] = None,
+                        W: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed causal attention: q [total, Hq, d], k/v [total, Hkv, d] (token-major, any token stride),
+    sequence b = tokens [cu[b], cu[b+1]).  Returns out [total, Hq, d]."""
+    _check_bf16("q", q, 3)
+    _check_bf16("k", k, 3)
+    _check_bf16("v", v, 3)
+    total, Hq, d = q.shape
+    Hkv = k.shape[1]
+    B = cu_seqlens.numel() - 1
+    if cu_seqlens.dtype != torch.int32 or not cu_seqlens.is_cuda or B <= 0:
+        raise ValueError("cu_seqlens must be a device int32 [B+1] tensor")
+    if out is None:
+        out = torch.empty((total, Hq, d), dtype=q.dtype, device=q.device)
+    bp, bsb, ep, esb, W = _bias_args(bias, enable, B, Hq, W)
+    flops, nbytes = prefill_work(1, Hq, Hkv, max_len, max_len, d, 0)
+    ev = TIMER.record("cram_prefill_varlen", flops * B, nbytes * B, q.device) if TIMER.enabled else None
+    code = _lib.load().cram_attn_prefill_varlen(
+        q.data_ptr(), q.stride(1), q.stride(0), k.data_ptr(), k.stride(1), k.stride(0),
+        v.data_ptr(), v.stride(1), v.stride(0), out.data_ptr(), out.stride(1), out.stride(0),
+        cu_seqlens.data_ptr(), B, int(max_len), Hq, Hkv, d, float(scale), bp, bsb, ep, esb, W, _stream(q.device))
+    _lib.check(code, "cram_attn_prefill_varlen")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(q.device))
+    return out
+
+
 def decode_workspace_bytes(B: int, Hq: int, d: int, num_splits: int) -> int:
     return int(_lib.load().cram_attn_decode_workspace_size(B, Hq, d, num_splits))
 

@@ -70,6 +70,18 @@ int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st,
                       cram_stream_t stream);
 
 /*
+ * Packed variable-length prefill (batched reweighted decode: many prompts in one GEMM pass).
+ * Sequence b occupies tokens [cu_seqlens[b], cu_seqlens[b+1]) of q/k/v/o, all laid out
+ * [token][head][d] with strides (x_st per token, x_sh per head); each sequence is causal from 0;
+ * bias row b applies to its own tokens.  max_len >= every sequence length.
+ */
+int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sh, int64_t k_st,
+                             const void* v, int64_t v_sh, int64_t v_st, void* o, int64_t o_sh, int64_t o_st,
+                             const int32_t* cu_seqlens, int B, int max_len, int Hq, int Hkv, int d, float scale,
+                             const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                             cram_stream_t stream);
+
+/*
  * Single-token decode attention (replaces the hooked SDPA call for q_len == 1;
  * reference: re_weighting.py:42-44 decode mask + :57-59 bias fill).
  *

@@ -55,6 +55,21 @@ def attn_decode(q, k, v, *, scale, seq_lens=None, bias=None, enable=None, W=0, n
     return o
 
 
+def attn_prefill_varlen(q, k, v, cu_seqlens, max_len, *, scale, bias=None, enable=None, W=0, out=None):
+    cu = cu_seqlens.tolist()
+    res = torch.empty(q.shape, dtype=q.dtype)
+    for b in range(len(cu) - 1):
+        a, e = cu[b], cu[b + 1]
+        o = attn_prefill(q[a:e].transpose(0, 1)[None], k[a:e].transpose(0, 1)[None], v[a:e].transpose(0, 1)[None],
+                         scale=scale, bias=None if bias is None else bias[b:b + 1],
+                         enable=None if enable is None else enable[b:b + 1], W=W)
+        res[a:e] = o[0]
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
 def answer_logits(hidden, w_lm, ids, *, round_bf16=False, out=None):
     r = (hidden.float() * w_lm[ids.long()].float()).sum(-1)
     if round_bf16:
@@ -94,8 +109,8 @@ def silu_mul(gu, F, out=None):
 def patched_ops():
     """Route cram_amd.ops through the CPU stand-ins for the duration of a CPU test."""
     from cram_amd import ops
-    names = ("attn_prefill", "attn_decode", "answer_logits", "decode_workspace_bytes", "rmsnorm", "rope_inplace",
-             "silu_mul")
+    names = ("attn_prefill", "attn_prefill_varlen", "attn_decode", "answer_logits", "decode_workspace_bytes",
+             "rmsnorm", "rope_inplace", "silu_mul")
     saved = {n: getattr(ops, n) for n in names}
     g = globals()
     for n in names:

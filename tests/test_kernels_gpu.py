@@ -211,3 +211,37 @@ def test_silu_mul_matches_transformers(gpu_device, F):
     got = ops.silu_mul(gu, F)
     ud = _ulp_diff(got, ref)
     assert ud.max() <= 1 and (ud == 0).float().mean() > 0.995, (ud.max().item(), (ud == 0).float().mean().item())
+
+
+@pytest.mark.parametrize("lens,Hq,Hkv", [([17, 300, 1, 129], 8, 2), ([900, 77], 32, 8), ([5, 6, 7], 7, 1)])
+def test_prefill_varlen_matches_oracle(gpu_device, lens, Hq, Hkv):
+    """Packed sequences (cu_seqlens) in one launch == each sequence through the oracle."""
+    from cram_amd import ops
+    gen = torch.Generator().manual_seed(sum(lens))
+    d = 128
+    total = sum(lens)
+    N = (Hq + 2 * Hkv) * d
+    y = torch.randn(total, N, generator=gen).to(torch.bfloat16)      # packed fused-QKV rows
+    q = y[:, :Hq * d].view(total, Hq, d)
+    k = y[:, Hq * d:(Hq + Hkv) * d].view(total, Hkv, d)
+    v = y[:, (Hq + Hkv) * d:].view(total, Hkv, d)
+    W = max(lens)
+    lw, bias, enable, heads = _bias_inputs(len(lens), Hq, W, W, gen)
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    refs = []
+    for b, n in enumerate(lens):
+        a, e = cu[b], cu[b + 1]
+        refs.append(hook_ref.biased_attention_ref(q[a:e].transpose(0, 1)[None], k[a:e].transpose(0, 1)[None],
+                                                  v[a:e].transpose(0, 1)[None], lw[b:b + 1, :n], [heads[b]],
+                                                  d ** -0.5)[0])
+    ref = torch.cat(refs, 0)
+    dev = gpu_device
+    yd = y.to(dev)
+    out = ops.attn_prefill_varlen(yd[:, :Hq * d].view(total, Hq, d), yd[:, Hq * d:(Hq + Hkv) * d].view(total, Hkv, d),
+                                  yd[:, (Hq + Hkv) * d:].view(total, Hkv, d),
+                                  torch.tensor(cu, dtype=torch.int32, device=dev), max(lens), scale=d ** -0.5,
+                                  bias=bias.to(dev), enable=enable.to(dev), W=W)
+    torch.cuda.synchronize()
+    _check(out, ref)
