@@ -62,12 +62,12 @@ struct PrefillParams {
   int B, Hq, Hkv, Tq, S, W, q_pos0;
   float scale_log2;  // softmax scale * log2(e)
   int nqb, nblocks;
+  int hp;             // query heads per workgroup (1, 2 or 4; divides the GQA group)
   const int32_t* cu;  // varlen: [B+1] token offsets of packed sequences (q/k/v/o batch strides unused)
 };
 
 template <int D>
 struct PrefillCfg {
-  static constexpr int BQ = 128;              // query rows per workgroup (4 waves x 32)
   static constexpr int BK = 64;               // keys per tile
   static constexpr int KSTR = D * 2 + 16;     // K image row stride (bytes): conflict-free ds_read_b128
   static constexpr int VSTR = D * 2 + 64;     // V image row stride (bytes): conflict-free ds_read_b64_tr_b16
@@ -90,13 +90,17 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  // a workgroup = hp query heads of ONE kv head (GQA group) x (4 / hp) waves of 32 query rows:
+  // every K/V tile staged in LDS feeds hp heads, and waves that share rows finish together
+  const int hp = p.hp, rw = 4 / hp, BQ = 32 * rw;
+  const int nhg = p.Hq / hp;
   const int qi_blk = wid % p.nqb;
   const int bh = wid / p.nqb;
-  const int hq = bh % p.Hq;
-  const int b = bh / p.Hq;
+  const int hg = bh % nhg;
+  const int b = bh / nhg;
   const int qblk = p.nqb - 1 - qi_blk;  // heaviest (longest causal range) first
   const int G = p.Hq / p.Hkv;
-  const int hkv = hq / G;
+  const int hkv = (hg * hp) / G;
 
   // per-sequence extent: uniform batch, or packed varlen sequences (cu_seqlens)
   int Tq = p.Tq, S = p.S, q_pos0 = p.q_pos0;
@@ -105,19 +109,25 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
     tok0 = p.cu[b];
     Tq = S = p.cu[b + 1] - (int)tok0;
     q_pos0 = 0;
-    if (qblk * C::BQ >= Tq) return;   // whole workgroup exits before any barrier
+    if (qblk * BQ >= Tq) return;   // whole workgroup exits before any barrier
   }
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, hh = lane >> 5;
-  const int q_row0 = qblk * C::BQ + wave * 32;
+  const int hq = hg * hp + wave % hp;
+  const int q_row0 = qblk * BQ + (wave / hp) * 32;
   const int qrow = q_row0 + r;
   const int qpos = q_pos0 + qrow;
 
   const __bf16* qb = p.q + b * p.q_sb + tok0 * p.q_st + hq * p.q_sh;
   const __bf16* kbase = p.k + b * p.k_sb + tok0 * p.k_st + hkv * p.k_sh;
   const __bf16* vbase = p.v + b * p.v_sb + tok0 * p.v_st + hkv * p.v_sh;
-  const bool en = (p.bias != nullptr) && (p.enable != nullptr) && p.enable[b * p.en_sb + hq] != 0;
-  const float* brow = en ? p.bias + b * p.bias_sb : nullptr;
+  // per-wave head enable; the workgroup stages the bias tile if any of its heads is enabled
+  const bool has_bias = (p.bias != nullptr) && (p.enable != nullptr);
+  const bool en = has_bias && p.enable[b * p.en_sb + hq] != 0;
+  bool en_any = false;
+  if (has_bias)
+    for (int j = 0; j < hp; ++j) en_any |= p.enable[b * p.en_sb + hg * hp + j] != 0;
+  const float* brow = en_any ? p.bias + b * p.bias_sb : nullptr;
 
   // Q as the B operand of S^T = K.Q^T: lane (r, hh) holds Q[qrow][16ks + 8hh .. +7]
   bf16x8 qf[D / 16];
@@ -131,7 +141,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
     }
   }
 
-  const int blk_last_q = min(qblk * C::BQ + C::BQ, Tq) - 1;
+  const int blk_last_q = min(qblk * BQ + BQ, Tq) - 1;
   const int kv_end = min(S, q_pos0 + blk_last_q + 1);
   const int nt = (kv_end + C::BK - 1) / C::BK;
   const bool wave_live = q_row0 < Tq;
@@ -166,7 +176,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       kst[i] = __builtin_amdgcn_raw_buffer_load_b128(ksrd, (int)koff[i], 0, 0);
       vst[i] = __builtin_amdgcn_raw_buffer_load_b128(vsrd, (int)voff[i], 0, 0);
     }
-    if (en && tid < C::BK) {
+    if (en_any && tid < C::BK) {
       const int wl = p.W - key0;
       const auto bsrd = __builtin_amdgcn_make_buffer_rsrc((void*)(brow + key0), (short)0, wl > 0 ? wl * 4 : 0,
                                                           0x00020000);
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       *reinterpret_cast<u32x4*>(base + ldsk[i]) = kst[i];
       *reinterpret_cast<u32x4*>(base + ldsv[i]) = vst[i];
     }
-    if (en && tid < C::BK) reinterpret_cast<float*>(base + C::K_BYTES + C::V_BYTES)[tid] = bst;
+    if (en_any && tid < C::BK) reinterpret_cast<float*>(base + C::K_BYTES + C::V_BYTES)[tid] = bst;
   };
 
   float m = kNegInf, l = 0.f;
@@ -517,8 +527,11 @@ inline bool m8(int64_t s) { return (s & 7) == 0; }
 template <int D>
 int launch_prefill(PrefillParams& p, hipStream_t stream) {
   using C = PrefillCfg<D>;
-  p.nqb = (p.Tq + C::BQ - 1) / C::BQ;
-  const int64_t nblocks = (int64_t)p.nqb * p.Hq * p.B;
+  const int G = p.Hq / p.Hkv;
+  p.hp = (G % 4 == 0) ? 4 : (G % 2 == 0) ? 2 : 1;
+  const int bq = 32 * (4 / p.hp);
+  p.nqb = (p.Tq + bq - 1) / bq;
+  const int64_t nblocks = (int64_t)p.nqb * (p.Hq / p.hp) * p.B;
   if (nblocks > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
   p.nblocks = (int)nblocks;
   hipLaunchKernelGGL(prefill_kernel<D>, dim3(p.nblocks), dim3(256), 0, stream, p);
