@@ -68,6 +68,8 @@ def main():
     ap.add_argument("--decode-batch", type=int, default=64)
     ap.add_argument("--decode-tokens", type=int, default=16)
     ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--scores", default="ideal", choices=["ideal", "gpt"],
+                    help="decode scores: ideal [0.1,1,1,1,1] or the NQ GPT truthful scores (RAG_test.py:89-105)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-units", type=int, default=2)
     ap.add_argument("--blas", default="hipblaslt", choices=["hipblas", "hipblaslt"])
@@ -76,7 +78,7 @@ def main():
 
     import torch
     from cram_amd import dist as cdist
-    from cram_amd import ops, spans, sweep
+    from cram_amd import ops, scores, spans, sweep
     from cram_amd.engine import CrAMEngine, ModelSpec, configure_blas
 
     rank, world, local = cdist.init(args.dist_backend)
@@ -174,8 +176,10 @@ def main():
             rec = data[qi]
             if args.config == 5:
                 paras, sc = long_context_paras(data, qi)
+            elif args.scores == "gpt" and "ori_fake_truthful_scores" in rec:
+                paras, sc = scores.assemble(rec)                            # normalised + re-ordered
             else:
-                paras, sc = rec["ori_fake"] + rec["reranked_dense_ctxs"], [0.1, 1, 1, 1, 1]
+                paras, sc = scores.assemble(rec, ideal=True, ideal_score=1)     # [0.1, 1, 1, 1, 1]
             _, enc, w, _ = spans.encode(tok, name, rec["question"], paras, sc, "")
             prompts.append(enc["input_ids"][0].to(dev))
             ws.append(w)
@@ -195,9 +199,10 @@ def main():
         T_mean = sum(p.numel() for p in prompts) / len(prompts)
         decode = {"metric": "questions/sec reweighted-decode", "value": world * B * reps / float(dt.item()),
                   "unit": "questions/s", "batch_per_gpu": B, "new_tokens": args.decode_tokens,
-                  "heads": heads_desc, "scores": "ideal: fake 0.1, others 1.0", "mean_prompt_tokens": round(T_mean, 1),
+                  "heads": heads_desc, "scores": ("GPT truthful, -min, /max, stable sort" if args.scores == "gpt" and dsname == "nq"
+                             else "ideal: fake 0.1, others 1.0"), "mean_prompt_tokens": round(T_mean, 1),
                   "seconds": float(dt.item()), "repeats": reps,
-                  "note": "per-prompt prefill + graph-replayed greedy steps, EOS ignored (random weights)"}
+                  "note": "packed varlen prefill + graph-replayed greedy steps, EOS ignored (random weights)"}
         log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s (T mean {T_mean:.0f})")
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1, config 3)
@@ -231,8 +236,11 @@ def main():
                         "hbm_gbs_algorithmic": round(kt["bytes"] / (kt["total_ms"] * 1e-3) / 1e9, 1)}
                 if os.path.exists(PMC_FILE):
                     pmc = json.load(open(PMC_FILE))
-                    roof["traffic"] = pmc.get("hbm_bytes_per_launch")
-                    roof["traffic_note"] = pmc.get("note")
+                    ratio = pmc["traffic_over_algorithmic"]
+                    roof["traffic"] = round(ratio * roof["algorithmic_bytes_per_launch"])
+                    roof["traffic_note"] = (f"HBM bytes/launch = PMC (FETCH_SIZEx2 + WRITE_SIZE, {pmc['source']}) "
+                                            f"/ algorithmic = {ratio:.4f} at the sweep shape B=33 T=962, x this run's "
+                                            f"algorithmic bytes per launch")
             step_tf = ie["flops"] / ie["elapsed"] / 1e12
             result.update({
                 "value": round(ie["value"], 3), "unit": "heads/s",
