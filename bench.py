@@ -170,7 +170,7 @@ def main():
             heads = json.load(open(os.path.join(REPO, "data", "selected_heads.json")))["nq__llama3"]["heads"]
             heads_desc = "nq/llama3 selected_heads top-894"
         B = args.decode_batch if args.config != 5 else min(args.decode_batch, 16)
-        prompts, ws = [], []
+        qs, ps, ss = [], [], []
         for j in range(B):
             qi = (rank * B + j) % len(data)
             rec = data[qi]
@@ -180,9 +180,14 @@ def main():
                 paras, sc = scores.assemble(rec)                            # normalised + re-ordered
             else:
                 paras, sc = scores.assemble(rec, ideal=True, ideal_score=1)     # [0.1, 1, 1, 1, 1]
-            _, enc, w, _ = spans.encode(tok, name, rec["question"], paras, sc, "")
-            prompts.append(enc["input_ids"][0].to(dev))
-            ws.append(w)
+            qs.append(rec["question"])
+            ps.append(paras)
+            ss.append(sc)
+        th = time.perf_counter()
+        encs = spans.encode_batch(tok, name, qs, ps, ss)                     # host: prompts -> ids + fp16 weights
+        host_ms = (time.perf_counter() - th) * 1e3
+        prompts = [ids.to(dev) for ids, _, _ in encs]
+        ws = [w for _, w, _ in encs]
         eng.generate(prompts[:2], ws[:2], heads, max_new_tokens=4)          # warm the graph path
         torch.cuda.synchronize()
         if world > 1:
@@ -202,6 +207,7 @@ def main():
                   "heads": heads_desc, "scores": ("GPT truthful, -min, /max, stable sort" if args.scores == "gpt" and dsname == "nq"
                              else "ideal: fake 0.1, others 1.0"), "mean_prompt_tokens": round(T_mean, 1),
                   "seconds": float(dt.item()), "repeats": reps,
+                  "host_encode_ms_per_question": round(host_ms / B, 3),
                   "note": "packed varlen prefill + graph-replayed greedy steps, EOS ignored (random weights)"}
         log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s (T mean {T_mean:.0f})")
 

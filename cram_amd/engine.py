@@ -211,13 +211,19 @@ class CrAMEngine:
         return h + self.mlp(x2, lw)
 
     def layer_rows(self, hbuf: torch.Tensor, B: int, T: int, l: int, cos, sin, bias=None, enable=None, W: int = 0,
-                   out_rows: Optional[int] = None) -> torch.Tensor:
-        """One decoder layer over a ROW buffer hbuf [Mp, D]: rows [0, B*T) are B sequences of T tokens,
-        rows beyond are alignment padding (GEMM M rounded up to the 256-row hipBLASLt/rocBLAS macro tile;
-        padding rows carry garbage and are never read back).  out_rows=n returns [B*n, D] (last n rows)."""
+                   out_rows: Optional[int] = None, delta: Optional[torch.Tensor] = None):
+        """One decoder layer over a ROW buffer: rows [0, B*T) are B sequences of T tokens, rows beyond are
+        alignment padding (GEMM M rounded up to the 256-row hipBLASLt/rocBLAS macro tile; padding rows carry
+        garbage and are never read back).  The layer input is hbuf [Mp, D], or hbuf + delta when the previous
+        layer's MLP output is still pending (the residual add then runs inside this layer's first RMSNorm).
+        Returns (h, mlp_out): the layer output is h + mlp_out, left for the next consumer to fuse.
+        out_rows=n returns [B*n, D] pairs (last n rows of every sequence)."""
         sp, lw = self.spec, self.layers[l]
         M = B * T
-        x = ops.rmsnorm(hbuf, lw.ln1, sp.eps)
+        if delta is None:
+            x = ops.rmsnorm(hbuf, lw.ln1, sp.eps)
+        else:
+            hbuf, x = ops.rmsnorm(delta, lw.ln1, sp.eps, residual=hbuf)
         y = F.linear(x, lw.wqkv, lw.bqkv)
         yr = y[:M]
         ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
@@ -237,7 +243,7 @@ class CrAMEngine:
                              bias=bias, enable=enable, W=W, out=a.view(B, n, sp.num_heads, sp.head_dim))
             hres = hbuf[:M].view(B, T, -1)[:, -n:].reshape(B * n, -1)
         h2, x2 = ops.rmsnorm(F.linear(a, lw.wo), lw.ln2, sp.eps, residual=hres)
-        return h2 + self.mlp(x2, lw)
+        return h2, self.mlp(x2, lw)
 
     @torch.no_grad()
     def forward_hidden(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None, out_rows: Optional[int] = None,

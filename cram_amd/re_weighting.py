@@ -117,11 +117,9 @@ class Re_Weighting_Strategy:
     def run_RAG_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
                       max_new_tokens: int = 100, use_graph: bool = True) -> List[tuple]:
         """Batched greedy decode on the engine (per-row lengths and bias); same (prompt, answer) per question."""
-        prompts, ws = [], []
-        for q, p, s in zip(questions, paras_list, scores_list):
-            enc, w = self.decode_with_special_attention(question=q, paras=p, scores=s)
-            prompts.append(enc["input_ids"][0])
-            ws.append(w.cpu())
+        encs = _spans.encode_batch(self.tokenizer, self.model_name, questions, paras_list, scores_list)
+        prompts = [ids.to(self.device) for ids, _, _ in encs]
+        ws = [w for _, w, _ in encs]
         kw = self._generate_kwargs()
         eos = kw.get("eos_token_id", self.model.generation_config.eos_token_id)
         eos = [eos] if isinstance(eos, int) else list(eos or [])

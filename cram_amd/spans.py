@@ -82,6 +82,72 @@ def weight_vector(T: int, spans: Sequence[Tuple[int, int]], scores: Sequence[flo
     return w
 
 
+def _tokenize_batch(tokenizer, texts: Sequence[str], add_special: bool):
+    """[(ids int64 [T], token char starts int64 [T])] — the fast tokenizer's Rust batch encoder when the
+    tokenizer has one (same ids/offsets as tokenizer(...), re_weighting.py:98), else tokenizer(...)."""
+    backend = getattr(tokenizer, "_tokenizer", None)
+    if backend is not None and hasattr(backend, "encode_batch"):
+        encs = backend.encode_batch(list(texts), add_special_tokens=add_special)
+        return [(np.asarray(e.ids, dtype=np.int64), np.asarray(e.offsets, dtype=np.int64).reshape(-1, 2)[:, 0])
+                for e in encs]
+    out = []
+    for t in texts:
+        e = tokenizer([t], return_offsets_mapping=True, add_special_tokens=add_special)
+        out.append((np.asarray(e["input_ids"][0], dtype=np.int64),
+                    np.asarray(e["offset_mapping"][0], dtype=np.int64).reshape(-1, 2)[:, 0]))
+    return out
+
+
+def encode_batch(tokenizer, model_name: str, questions: Sequence[str], paras_list: Sequence[Sequence[str]],
+                 scores_list: Sequence[Sequence[float]], answers: Sequence[str] = None):
+    """Batched encode(): [(input_ids int64 [T], fp16 weight [1, T], spans)] per prompt.
+
+    One batch tokenizer call, str.find for the passage character ranges, then the native span builder
+    (cram_passage_weights in libcram_attn.so) for spans and fp16 weights of every prompt at once.
+    """
+    from . import _lib
+    n = len(questions)
+    answers = [""] * n if answers is None else list(answers)
+    texts, flags, lo, hi, sc, cu_par = [], [], [], [], [], [0]
+    for q, paras, scores, a in zip(questions, paras_list, scores_list, answers):
+        if len(scores) < len(paras):
+            raise IndexError("fewer scores than passages (the reference raises the same way at re_weighting.py:111)")
+        text, add_special = build_prompt(tokenizer, model_name, list(paras), q, a)
+        texts.append(text)
+        flags.append(add_special)
+        for i, p in enumerate(paras):
+            para = passage_text(i, p) + "\n"
+            c0 = text.find(para)
+            lo.append(c0)
+            hi.append(c0 + len(para) - 1)
+        sc.extend(float(x) for x in scores[:len(paras)])
+        cu_par.append(len(lo))
+    if len(set(flags)) > 1:
+        raise ValueError("mixed special-token settings in one batch")
+    toks = _tokenize_batch(tokenizer, texts, flags[0] if flags else True)
+    cu_tok = np.zeros(n + 1, dtype=np.int64)
+    cu_tok[1:] = np.cumsum([len(ids) for ids, _ in toks])
+    starts = np.concatenate([st for _, st in toks]) if n else np.zeros(0, np.int64)
+    cu_par = np.asarray(cu_par, dtype=np.int64)
+    lo = np.asarray(lo, dtype=np.int64)
+    hi = np.asarray(hi, dtype=np.int64)
+    sc32 = np.asarray(sc, dtype=np.float64).astype(np.float32)           # score -> fp32 -> fp16 (re_weighting.py:110)
+    span_lo = np.empty(len(lo), dtype=np.int32)
+    span_hi = np.empty(len(lo), dtype=np.int32)
+    w16 = np.empty(int(cu_tok[-1]), dtype=np.float16)
+    ptr = lambda a: a.ctypes.data if a.size else None
+    rc = _lib.load().cram_passage_weights(n, ptr(cu_tok), ptr(starts), ptr(cu_par), ptr(lo), ptr(hi), ptr(sc32),
+                                          ptr(span_lo), ptr(span_hi), ptr(w16))
+    if rc != 0:
+        raise ValueError("a passage is not in its prompt (re_weighting.py:102-110 fails the same way)")
+    out = []
+    for b in range(n):
+        t0, t1 = int(cu_tok[b]), int(cu_tok[b + 1])
+        sp = list(zip(span_lo[cu_par[b]:cu_par[b + 1]].tolist(), span_hi[cu_par[b]:cu_par[b + 1]].tolist()))
+        out.append((torch.from_numpy(toks[b][0]), torch.from_numpy(w16[t0:t1].copy()).view(1, -1), sp))
+    return out
+
+
 def encode(tokenizer, model_name: str, question: str, paras: Sequence[str], scores: Sequence[float],
            answer: str = ""):
     """(text, input_ids [1,T] int64, fp16 weight [1,T], spans) for one question, on the host."""

@@ -105,12 +105,14 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
     hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
     h, x2 = ops.rmsnorm(F.linear(abuf, lw.wo), lw.ln2, sp.eps, residual=hin)   # [Mp, D]
-    h = h + eng.mlp(x2, lw)
+    m = eng.mlp(x2, lw)                                                 # layer output h + m, add deferred
     if not last:
         cos, sin = eng.rope_tables(T)
         for l2 in range(l + 1, L):
-            h = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None)
-    return eng.rmsnorm(h[:Hv * n_ans], eng.norm).view(Hv, n_ans, sp.hidden)   # [Hv, n, D]
+            h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m)
+    rows = Hv * n_ans
+    _, y = ops.rmsnorm(m[:rows], eng.norm, sp.eps, residual=h[:rows])   # final norm of h + m
+    return y.view(Hv, n_ans, sp.hidden)                                 # [Hv, n, D]
 
 
 @torch.no_grad()

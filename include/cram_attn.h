@@ -130,6 +130,24 @@ int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads,
                       const void* sin_t, int64_t tab_rs, const int64_t* pos, cram_stream_t stream);
 int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, cram_stream_t stream);
 
+/*
+ * Host-side prompt -> credibility weights (cram_spans.cpp; no device, no stream), batched over B prompts.
+ * Replaces the per-passage offset-mapping scan of re_weighting.py:100-111.
+ *
+ *   tok_start [cu_tok[B]]  character start of every token (offset_mapping[:, 0]), prompt b's tokens at
+ *                          [cu_tok[b], cu_tok[b+1])
+ *   char_lo/char_hi/score [cu_par[B]]  passage p of prompt b (p in [cu_par[b], cu_par[b+1])): index of
+ *                          "Passage-i: " in the prompt (prompt.find, re_weighting.py:102) and of its
+ *                          trailing '\n' (:103); the passage's score as fp32
+ *   span_lo/span_hi [cu_par[B]]  out: max{t : tok_start[t] <= char_lo} and max{t : tok_start[t] <= char_hi}
+ *                          (token indices within the prompt, inclusive span, :105-109)
+ *   w16 [cu_tok[B]]        out: fp16 bits, fp16(score) over each span (later passages overwrite), 1.0 elsewhere
+ * Returns CRAM_ERR_INVALID_ARG for a passage that was not found (char_lo < 0) or precedes every token.
+ */
+int cram_passage_weights(int B, const int64_t* cu_tok, const int64_t* tok_start, const int64_t* cu_par,
+                         const int64_t* char_lo, const int64_t* char_hi, const float* score,
+                         int32_t* span_lo, int32_t* span_hi, uint16_t* w16);
+
 #ifdef __cplusplus
 }
 #endif

@@ -154,3 +154,46 @@ def test_missing_passage_raises(toks):
         S.token_spans("no passages here", ["abc"], [(0, 2), (3, 5)])
     with pytest.raises(IndexError):
         S.encode(toks["llama3"], NAMES["llama3"], "q?", ["a", "b"], [1.0])
+
+
+def test_spans_native_batch_bit_exact(span_rows, toks):
+    """encode_batch (batch tokenizer + cram_passage_weights in libcram_attn.so) vs the reference's vectors."""
+    for kind in ("llama3", "qwen2"):
+        rows = [r for r in span_rows if r["kind"] == kind]
+        out = S.encode_batch(toks[kind], NAMES[kind], [r["question"] for r in rows], [r["paras"] for r in rows],
+                             [r["scores"] for r in rows], [r["answer"] for r in rows])
+        for r, (ids, w, sp) in zip(rows, out):
+            assert ids.tolist() == r["input_ids"], (kind, r["ds"], r["idx"], r["variant"])
+            assert w[0].float().tolist() == r["weight"], (kind, r["ds"], r["idx"], r["variant"])
+
+
+def test_native_span_rule_edge_cases():
+    """cram_passage_weights directly: non-monotone offsets, overlap order, fp16 rounding, errors."""
+    from cram_amd import _lib
+    L = _lib.load()
+
+    def run(starts, lo, hi, sc):
+        cu_tok = np.array([0, len(starts)], np.int64)
+        cu_par = np.array([0, len(lo)], np.int64)
+        st = np.asarray(starts, np.int64)
+        lo_, hi_ = np.asarray(lo, np.int64), np.asarray(hi, np.int64)
+        s = np.asarray(sc, np.float32)
+        a, e = np.zeros(len(lo), np.int32), np.zeros(len(lo), np.int32)
+        w = np.zeros(len(starts), np.float16)
+        rc = L.cram_passage_weights(1, cu_tok.ctypes.data, st.ctypes.data, cu_par.ctypes.data, lo_.ctypes.data,
+                                    hi_.ctypes.data, s.ctypes.data, a.ctypes.data, e.ctypes.data, w.ctypes.data)
+        return rc, list(zip(a.tolist(), e.tolist())), w
+
+    # the reference's scan takes the LAST token whose start <= c, also when offsets are not monotone
+    starts = [0, 0, 5, 9, 0, 14, 20]
+    rc, sp, w = run(starts, [9], [19], [0.1])
+    ref = [max(t for t, x in enumerate(starts) if x <= c) for c in (9, 19)]
+    assert rc == 0 and sp == [tuple(ref)] == [(4, 5)]
+    assert w.tolist() == [1, 1, 1, 1, np.float16(0.1), np.float16(0.1), 1]
+    # overlapping spans: later passage wins; fp32 -> fp16 rounding of the score
+    rc, sp, w = run([0, 3, 6, 9, 12], [3, 6], [8, 13], [0.3, 1 / 3])
+    assert rc == 0 and sp == [(1, 2), (2, 4)]
+    assert w.view(np.uint16).tolist()[1:] == [np.float16(0.3).view(np.uint16), *[np.float16(np.float32(1 / 3))
+                                                                                  .view(np.uint16)] * 3]
+    assert run([0, 3], [-1], [5], [1.0])[0] == -1          # passage not found
+    assert run([4, 8], [2], [9], [1.0])[0] == -1           # precedes every token
