@@ -23,7 +23,6 @@ from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
 from .bias import CredibilityBias
@@ -175,13 +174,13 @@ class CrAMEngine:
         return (emb.cos() * self.attn_scaling).to(self.dtype), (emb.sin() * self.attn_scaling).to(self.dtype)
 
     def mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
-        gu = F.linear(x, lw.wgu)
-        return F.linear(ops.silu_mul(gu, self.spec.intermediate), lw.wd)
+        gu = ops.linear(x, lw.wgu)
+        return ops.linear(ops.silu_mul(gu, self.spec.intermediate), lw.wd)
 
     def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin, pos: Optional[torch.Tensor] = None):
         """x [B, T, D] -> roped q [B, T, Hq, d], k / v [B, T, Hkv, d]: strided views of one fused buffer."""
         sp = self.spec
-        y = F.linear(x, lw.wqkv, lw.bqkv)
+        y = ops.linear(x, lw.wqkv, lw.bqkv)
         ops.rope_inplace(y, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=y.shape[-2], pos=pos)
         q = y[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
         k = y[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
@@ -207,7 +206,7 @@ class CrAMEngine:
             q = q[:, -out_rows:]
             h = h[:, -out_rows:]
         a = self.attention(q, k, v, bias, enable, W)
-        h, x2 = self.add_rmsnorm(F.linear(a.flatten(-2), lw.wo), h, lw.ln2)
+        h, x2 = self.add_rmsnorm(ops.linear(a.flatten(-2), lw.wo), h, lw.ln2)
         return h + self.mlp(x2, lw)
 
     def layer_rows(self, hbuf: torch.Tensor, B: int, T: int, l: int, cos, sin, bias=None, enable=None, W: int = 0,
@@ -224,7 +223,7 @@ class CrAMEngine:
             x = ops.rmsnorm(hbuf, lw.ln1, sp.eps)
         else:
             hbuf, x = ops.rmsnorm(delta, lw.ln1, sp.eps, residual=hbuf)
-        y = F.linear(x, lw.wqkv, lw.bqkv)
+        y = ops.linear(x, lw.wqkv, lw.bqkv)
         yr = y[:M]
         ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
         y3 = yr.view(B, T, -1)
@@ -242,7 +241,7 @@ class CrAMEngine:
             ops.attn_prefill(q[:, -n:].transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale,
                              bias=bias, enable=enable, W=W, out=a.view(B, n, sp.num_heads, sp.head_dim))
             hres = hbuf[:M].view(B, T, -1)[:, -n:].reshape(B * n, -1)
-        h2, x2 = ops.rmsnorm(F.linear(a, lw.wo), lw.ln2, sp.eps, residual=hres)
+        h2, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=hres)
         return h2, self.mlp(x2, lw)
 
     @torch.no_grad()
@@ -264,7 +263,7 @@ class CrAMEngine:
     @torch.no_grad()
     def logits(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None, last: Optional[int] = None):
         h = self.forward_hidden(ids, cb, out_rows=last)
-        return F.linear(h, self.lm_head)
+        return ops.linear(h, self.lm_head)
 
     def answer_logits(self, hidden: torch.Tensor, ids: torch.Tensor, round_bf16: bool = False) -> torch.Tensor:
         """hidden [n, D] bf16, ids int32 [n] -> fp32 [n] (HIP gather-dot)."""
@@ -367,7 +366,7 @@ class DecodeSession:
             h[total:].zero_()
         for l, lw in enumerate(eng.layers):
             x = ops.rmsnorm(h, lw.ln1, sp.eps)
-            y = F.linear(x, lw.wqkv, lw.bqkv)
+            y = ops.linear(x, lw.wqkv, lw.bqkv)
             yr = y[:total]
             ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, self.cos, self.sin, T=1, pos=pos)
             q = yr[:, :sp.q_size].view(total, sp.num_heads, sp.head_dim)
@@ -381,10 +380,10 @@ class DecodeSession:
             ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=self.cb.bias,
                                     enable=self.cb.enable[l], W=self.cb.W,
                                     out=a[:total].view(total, sp.num_heads, sp.head_dim))
-            h, x2 = ops.rmsnorm(F.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
+            h, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
             h = h + eng.mlp(x2, lw)
         hn = eng.rmsnorm(h[cu[1:].long() - 1], eng.norm)
-        self.tokens.copy_(self._pick(F.linear(hn, eng.lm_head)))
+        self.tokens.copy_(self._pick(ops.linear(hn, eng.lm_head)))
         self.out[:, 0] = self.tokens
         self.t.fill_(1)
 
@@ -399,7 +398,7 @@ class DecodeSession:
 
             sub = CredibilityBias(self.cb.bias[b:b + 1], self.cb.enable[:, b:b + 1], self.cb.W)
             h = eng.forward_hidden(ids[None], sub, out_rows=1, kv_out=kv_out)
-            self.tokens[b] = self._pick(F.linear(h[0, -1], eng.lm_head))
+            self.tokens[b] = self._pick(ops.linear(h[0, -1], eng.lm_head))
         self.out[:, 0] = self.tokens
         self.t.fill_(1)
 
@@ -415,10 +414,10 @@ class DecodeSession:
             a = ops.attn_decode(q[:, 0], self.k_cache[l], self.v_cache[l], scale=eng.scale, seq_lens=self.seq_lens,
                                 bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
                                 workspace=self.ws)
-            h, x2 = eng.add_rmsnorm(F.linear(a.flatten(-2)[:, None], lw.wo), h, lw.ln2)
+            h, x2 = eng.add_rmsnorm(ops.linear(a.flatten(-2)[:, None], lw.wo), h, lw.ln2)
             h = h + eng.mlp(x2, lw)
         hn = eng.rmsnorm(h[:, 0], eng.norm)
-        nxt = self._pick(F.linear(hn, eng.lm_head))
+        nxt = self._pick(ops.linear(hn, eng.lm_head))
         self.tokens.copy_(nxt)
         self.out.index_copy_(1, self.t.view(1), nxt[:, None])
         self.t.add_(1)

@@ -58,6 +58,18 @@ def prefill_work(B, Hq, Hkv, Tq, S, d, q_pos0):
     return flops, nbytes
 
 
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """F.linear (hipBLASLt / rocBLAS GEMM), timed as "gemm" when the bench's KernelTimer is on."""
+    if not TIMER.enabled:
+        return torch.nn.functional.linear(x, w, b)
+    M = x.numel() // x.shape[-1]
+    N, K = w.shape
+    ev = TIMER.record("gemm", 2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), x.device)
+    y = torch.nn.functional.linear(x, w, b)
+    ev.record(torch.cuda.current_stream(x.device))
+    return y
+
+
 def _stream(dev: torch.device) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 

@@ -114,6 +114,32 @@ class Re_Weighting_Strategy:
         return prompt, output
 
     @torch.no_grad()
+    def answer_logprobs(self, question: str = "", paras: list = (), scores: list = (), answer: str = "",
+                        n_answer: Optional[int] = None) -> torch.Tensor:
+        """Re-weighted teacher-forced log-probabilities of the answer tokens, fp32 [n] on the device.
+
+        Prompt + answer is encoded as decode_with_special_attention(answer=...) does (re_weighting.py:63-113);
+        one forward of the model with the credibility bias on layers_to_be_modified (the hooked forward of
+        re_weighting.py:118-127) gives logits; token T-n+k is scored by log_softmax(logits[T-n-1+k]).
+        n defaults to the reference's answer length convention (tokenize([answer])[0, 1:], :155).
+        Not a reference method: it exposes the quantity the parity tests hold to a tolerance.
+        """
+        if n_answer is None:
+            n_answer = int(self.tokenizer([answer], return_tensors="pt")["input_ids"].shape[1]) - 1
+        model_inputs, w = self.decode_with_special_attention(question=question, paras=paras, scores=scores,
+                                                             answer=answer)
+        ids = model_inputs["input_ids"]
+        T = ids.shape[1]
+        n = max(0, min(int(n_answer), T - 1))
+        if n == 0:
+            return torch.zeros(0, dtype=torch.float32, device=self.device)
+        cb = self._bias(w, self.layers_to_be_modified)
+        with _attn.reweighting(self.model, cb):
+            logits = self.model(input_ids=ids, logits_to_keep=n + 1).logits[0, :n]        # rows T-n-1 .. T-2
+        lp = torch.log_softmax(logits.float(), dim=-1)
+        return lp.gather(1, ids[0, T - n:].view(n, 1)).view(n)
+
+    @torch.no_grad()
     def run_RAG_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
                       max_new_tokens: int = 100, use_graph: bool = True) -> List[tuple]:
         """Batched greedy decode on the engine (per-row lengths and bias); same (prompt, answer) per question."""
@@ -165,6 +191,16 @@ class Find_Best_Heads(Re_Weighting_Strategy):
             return torch.zeros((L, H), dtype=torch.float32, device=self.device)
         return _sweep.ie_question(self.engine, model_inputs["input_ids"][0], w[0].cpu(), ans,
                                   round_bf16_logits=round_bf16_logits)
+
+    @torch.no_grad()
+    def cal_logits_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
+                         wrong_answers: List[str], round_bf16_logits: bool = False) -> torch.Tensor:
+        """IE of many questions as one device tensor [Nq, L, H] fp32 (the sweep's batched form)."""
+        out = torch.empty((len(questions), self.model_num_hidden_layers, self.model_num_attention_heads),
+                          dtype=torch.float32, device=self.device)
+        for i, (q, p, s, a) in enumerate(zip(questions, paras_list, scores_list, wrong_answers)):
+            out[i] = self.cal_logits_tensor(q, p, s, "", a, round_bf16_logits)
+        return out
 
     def cal_logits(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
                    wrong_answer: str = "my name is") -> list:

@@ -30,7 +30,6 @@ from __future__ import annotations
 from typing import Optional
 
 import torch
-import torch.nn.functional as F
 
 from . import ops
 from .bias import CredibilityBias
@@ -71,7 +70,7 @@ def baseline(eng: CrAMEngine, ids: torch.Tensor, n_ans: int, keep: bool = True):
         if l == L - 1:
             a = a[:, -n_ans:]
             h = h[:, -n_ans:]
-        h, x2 = eng.add_rmsnorm(F.linear(a.flatten(-2), lw.wo), h, lw.ln2)
+        h, x2 = eng.add_rmsnorm(ops.linear(a.flatten(-2), lw.wo), h, lw.ln2)
         h = h + eng.mlp(x2, lw)
     return eng.rmsnorm(h, eng.norm)[0], qc
 
@@ -104,7 +103,7 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     lw = eng.layers[l]
     hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
     hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
-    h, x2 = ops.rmsnorm(F.linear(abuf, lw.wo), lw.ln2, sp.eps, residual=hin)   # [Mp, D]
+    h, x2 = ops.rmsnorm(ops.linear(abuf, lw.wo), lw.ln2, sp.eps, residual=hin)   # [Mp, D]
     m = eng.mlp(x2, lw)                                                 # layer output h + m, add deferred
     if not last:
         cos, sin = eng.rope_tables(T)

@@ -174,6 +174,21 @@ def answer_logit_sum(logits: torch.Tensor, answer_ids: torch.Tensor) -> torch.Te
 
 
 @torch.no_grad()
+def answer_logprobs(model, input_ids: torch.Tensor, lw: torch.Tensor, layers_to_heads: dict, n: int) -> torch.Tensor:
+    """Hooked forward (re_weighting.py:118-127 hooks, :36-61 mask) -> fp32 log_softmax of token T-n+k at
+    row T-n-1+k, k < n (teacher-forced answer log-probabilities under re-weighting)."""
+    hs = register_hooks(model, layers_to_heads, lw)
+    try:
+        lg = model(input_ids=input_ids, attention_mask=torch.ones_like(input_ids), return_dict=True)["logits"]
+    finally:
+        for x in hs:
+            x.remove()
+    T = input_ids.shape[1]
+    lp = torch.log_softmax(lg[0, T - n - 1:T - 1].float(), dim=-1)
+    return lp.gather(1, input_ids[0, T - n:].view(n, 1)).view(n)
+
+
+@torch.no_grad()
 def ie_grid(model, input_ids: torch.Tensor, lw: torch.Tensor, answer_ids: torch.Tensor,
             layers: Optional[Sequence[int]] = None, heads: Optional[Sequence[int]] = None,
             upcast_logits: bool = False) -> np.ndarray:

@@ -16,6 +16,7 @@ Outputs (data only) in tests/golden/:
   tiny_ie.json.gz   G4  cal_logits IE grids (bf16 logits and fp32 logits) + baseline answer logits
   tiny_ie_f32.json.gz G4' cal_logits on the float32 copy of the same weights (IE ground truth)
   generate.json.gz  G5  run_RAG_with_attention_weighting outputs + greedy ids + hooked last-row logits
+  logprobs.json.gz  G6  re-weighted answer-token log-probabilities through the reference hook (bf16 + fp32 copies)
 """
 import contextlib
 import gzip
@@ -225,9 +226,55 @@ def gen_generate(rw):
         json.dump(res, f)
 
 
+def gen_logprobs(rw):
+    """Re-weighted teacher-forced answer log-probabilities through the reference's own hook
+    (Re_Weighting_Strategy.edit_attention_mask registered exactly as re_weighting.py:119-123 does),
+    for the bf16 tiny models and their float32 copies (the ground truth)."""
+    from functools import partial
+    res = []
+    recs = load_data("nq")[:3]
+    for kind in ("llama3", "qwen2"):
+        for fp32 in (False, True):
+            path = tm.save_model(kind, MODEL_ROOT, fp32=fp32)
+            with cuda_to_cpu():
+                obj = rw.Re_Weighting_Strategy(model_name=path, layers_to_be_modified={}, bad_words_ids=[])
+            L, H = obj.model.config.num_hidden_layers, obj.model.config.num_attention_heads
+            head_sets = {"sel": {0: [1], 1: [0, H - 1], L - 1: [H - 1]},
+                         "all": {l: list(range(H)) for l in range(L)}}
+            for i, rec in enumerate(recs):
+                paras = rec["ori_fake"] + rec["reranked_dense_ctxs"]
+                n = obj.tokenizer([rec["wrong_answer"]], return_tensors="pt")["input_ids"].shape[1] - 1
+                for sname, scores in (("ideal", [0.1, 1, 1, 1, 1]), ("sweep", [0, 1, 1, 1, 1])):
+                    with cuda_to_cpu():
+                        mi, aw = obj.decode_with_special_attention(question=rec["question"], paras=paras,
+                                                                   scores=scores, answer=rec["wrong_answer"])
+                    ids = mi["input_ids"]
+                    T = ids.shape[1]
+                    for hname, heads in head_sets.items():
+                        hooks = []
+                        for layer_idx, head_idx in heads.items():
+                            module = obj.model.get_submodule(f"model.layers.{layer_idx}.self_attn")
+                            hooks.append(module.register_forward_pre_hook(
+                                partial(obj.edit_attention_mask, attention_weight=torch.log(aw), head_idx=head_idx),
+                                with_kwargs=True))
+                        with torch.no_grad(), cuda_to_cpu():
+                            lg = obj.model(**mi).logits
+                        for hk in hooks:
+                            hk.remove()
+                        lp = torch.log_softmax(lg[0, T - n - 1:T - 1].float(), dim=-1)
+                        lp = lp.gather(1, ids[0, T - n:].view(n, 1)).view(n)
+                        res.append({"kind": kind, "fp32": fp32, "idx": i, "scores": sname, "heads": hname,
+                                    "layers_to_heads": {str(k): v for k, v in heads.items()}, "n": n,
+                                    "ids": ids[0].tolist(), "logprobs": lp.tolist()})
+                        print(kind, fp32, i, sname, hname, [round(x, 4) for x in lp.tolist()])
+            del obj
+    with gzip.open(os.path.join(OUT, "logprobs.json.gz"), "wt", encoding="utf-8") as f:
+        json.dump(res, f)
+
+
 def main():
     import re_weighting as rw  # the reference module, unmodified
-    which = sys.argv[1:] or ["spans", "masks", "ie", "ie32", "generate"]
+    which = sys.argv[1:] or ["spans", "masks", "ie", "ie32", "generate", "logprobs"]
     if "spans" in which:
         gen_spans(rw)
     if "masks" in which:
@@ -238,6 +285,8 @@ def main():
         gen_ie_f32(rw)
     if "generate" in which:
         gen_generate(rw)
+    if "logprobs" in which:
+        gen_logprobs(rw)
 
 
 if __name__ == "__main__":

@@ -195,3 +195,45 @@ def test_batched_sweep_equals_unbatched_on_gpu(fbh, nq):
     un = np.array([[ori - s(CredibilityBias.build([w.cpu()], {l: [h]}, L, H, gpu)) for h in range(H)] for l in range(L)])
     sw = sweep.ie_question(eng, ids[0], w[0].cpu(), ans.cpu()).double().cpu().numpy()
     assert np.abs(sw - un).max() < 0.05, np.abs(sw - un).max()
+
+
+@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+def test_answer_logprobs_match_reference_hook(paths, nq, gpu_device, kind):
+    """G6: re-weighted answer-token log-probabilities through the drop-in (transformers model + cram_hip
+    attention) vs the reference hook path.  Bar: per token |ours - fp32 truth| <= 2.5 x the reference's own
+    bf16 error on that sample + 0.01 (truth = the reference hook on the float32 copy of the weights)."""
+    from cram_amd.re_weighting import Re_Weighting_Strategy
+    rows = [r for r in _load("logprobs.json.gz") if r["kind"] == kind]
+    truth = {(r["idx"], r["scores"], r["heads"]): np.array(r["logprobs"]) for r in rows if r["fp32"]}
+    objs = {}
+    worst = 0.0
+    for r in rows:
+        if r["fp32"]:
+            continue
+        if r["heads"] not in objs:
+            objs[r["heads"]] = Re_Weighting_Strategy(model_name=paths[kind],
+                                                     layers_to_be_modified=r["layers_to_heads"])
+        obj = objs[r["heads"]]
+        rec = nq[r["idx"]]
+        scores = [0.1, 1, 1, 1, 1] if r["scores"] == "ideal" else [0, 1, 1, 1, 1]
+        lp = obj.answer_logprobs(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
+                                 scores=scores, answer=rec["wrong_answer"])
+        assert lp.is_cuda and lp.dtype == torch.float32 and lp.numel() == r["n"]
+        t = truth[(r["idx"], r["scores"], r["heads"])]
+        ref_err = np.abs(np.array(r["logprobs"]) - t).max()
+        err = np.abs(lp.cpu().numpy() - t)
+        assert err.max() <= 2.5 * ref_err + 0.01, (kind, r["idx"], r["scores"], r["heads"], err.max(), ref_err)
+        worst = max(worst, err.max() / (ref_err + 1e-3))
+    print(f"{kind}: worst error / reference bf16 error = {worst:.2f}")
+
+
+def test_cal_logits_batch_equals_per_question(fbh, nq):
+    obj = fbh["qwen2"]
+    recs = nq[:3]
+    args = ([r["question"] for r in recs], [r["ori_fake"] + r["reranked_dense_ctxs"] for r in recs],
+            [[0, 1, 1, 1, 1]] * 3, [r["wrong_answer"] for r in recs])
+    batch = obj.cal_logits_batch(*args)
+    assert batch.shape == (3, obj.model_num_hidden_layers, obj.model_num_attention_heads) and batch.is_cuda
+    for i, r in enumerate(recs):
+        one = obj.cal_logits_tensor(args[0][i], args[1][i], [0, 1, 1, 1, 1], "", args[3][i])
+        assert torch.equal(batch[i], one)

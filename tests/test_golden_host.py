@@ -197,3 +197,34 @@ def test_native_span_rule_edge_cases():
                                                                                   .view(np.uint16)] * 3]
     assert run([0, 3], [-1], [5], [1.0])[0] == -1          # passage not found
     assert run([4, 8], [2], [9], [1.0])[0] == -1           # precedes every token
+
+
+@pytest.fixture(scope="module")
+def logprob_rows():
+    with gzip.open(os.path.join(GOLD, "logprobs.json.gz"), "rt", encoding="utf-8") as f:
+        return json.load(f)
+
+
+def test_oracle_answer_logprobs_bit_exact(logprob_rows, tmp_path_factory):
+    """G6: the oracle's hook restatement on the same transformers model reproduces the reference hook's
+    re-weighted answer log-probabilities exactly (bf16 and fp32 tiny models)."""
+    from transformers import AutoModelForCausalLM, AutoTokenizer
+    root = str(tmp_path_factory.mktemp("tinylp"))
+    with gzip.open(os.path.join(tm.REPO, "data", "nq_1000.json.gz"), "rt") as f:
+        nq = json.load(f)
+    models, toks_ = {}, {}
+    for r in logprob_rows:
+        key = (r["kind"], r["fp32"])
+        if key not in models:
+            path = tm.save_model(r["kind"], root, fp32=r["fp32"])
+            models[key] = AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval()
+            toks_[key] = (AutoTokenizer.from_pretrained(path), path)
+        tok, path = toks_[key]
+        rec = nq[r["idx"]]
+        scores = [0.1, 1, 1, 1, 1] if r["scores"] == "ideal" else [0, 1, 1, 1, 1]
+        _, enc, w, _ = S.encode(tok, path, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"], scores,
+                                rec["wrong_answer"])
+        assert enc["input_ids"][0].tolist() == r["ids"]
+        heads = {int(k): v for k, v in r["layers_to_heads"].items()}
+        lp = hook_ref.answer_logprobs(models[key], torch.tensor([r["ids"]]), hook_ref.log_weight(w), heads, r["n"])
+        assert lp.tolist() == r["logprobs"], (r["kind"], r["fp32"], r["idx"], r["scores"], r["heads"])
