@@ -46,6 +46,20 @@ __device__ __forceinline__ float half_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// sum over the LPK-lane group of a key row (LPK = 16 or 8) with DPP lane swaps inside a 16-lane row:
+// xor 1, xor 2 (quad_perm), then the half-row and row mirrors pair every quad with the others
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int LPK>
+__device__ __forceinline__ float group_sum(float x) {
+  x += dpp_mov<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_mov<0x141>(x);   // row_half_mirror: lane i <-> 7-i within each 8 lanes
+  if constexpr (LPK == 16) x += dpp_mov<0x140>(x);   // row_mirror: lane i <-> 15-i
+  return x;
+}
 __device__ __forceinline__ float half_sum(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -408,21 +422,35 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
     for (int j = 0; j < 8; ++j) acc[g][j] = 0.f;
   }
 
+  // K/V rows of the next iteration are loaded while the current one is computed (register double
+  // buffer): every wave keeps 2 x U x 2 16-byte loads in flight instead of stalling on each batch
+  bf16x8 kn[U], vn[U];
+  auto load_keys = [&](int kb0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int key = kb0 + u * STEP;
+      if (key < k_end) {
+        kn[u] = *reinterpret_cast<const bf16x8*>(kbase + key * p.k_st);
+        vn[u] = *reinterpret_cast<const bf16x8*>(vbase + key * p.v_st);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kn[u][j] = (__bf16)0.f; vn[u][j] = (__bf16)0.f; }
+      }
+    }
+  };
+  constexpr bool PF = G <= 4;   // larger head groups keep two waves per SIMD instead (VGPR budget)
+  if (PF) load_keys(k_begin + wave * KPW + grp);
   for (int key_base = k_begin + wave * KPW + grp; key_base < k_end; key_base += U * STEP) {
+    if (!PF) load_keys(key_base);
     bf16x8 kr[U], vr[U];
     bool valid[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int key = key_base + u * STEP;
-      valid[u] = key < k_end;
-      if (valid[u]) {
-        kr[u] = *reinterpret_cast<const bf16x8*>(kbase + key * p.k_st);
-        vr[u] = *reinterpret_cast<const bf16x8*>(vbase + key * p.v_st);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { kr[u][j] = (__bf16)0.f; vr[u][j] = (__bf16)0.f; }
-      }
+      kr[u] = kn[u];
+      vr[u] = vn[u];
+      valid[u] = key_base + u * STEP < k_end;
     }
+    if (PF && key_base + U * STEP < k_end) load_keys(key_base + U * STEP);
     float bias_u[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -437,8 +465,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
         float d = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) d += qv[g][j] * (float)kr[u][j];
-#pragma unroll
-        for (int off = LPK / 2; off >= 1; off >>= 1) d += __shfl_xor(d, off, 64);
+        d = group_sum<LPK>(d);
         s[u] = valid[u] ? d + (en[g] ? bias_u[u] : 0.f) : kNegInf;
       }
       float mx = s[0];
