@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--scores", default="ideal", choices=["ideal", "gpt"],
                     help="decode scores: ideal [0.1,1,1,1,1] or the NQ GPT truthful scores (RAG_test.py:89-105)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prefix-skip", action="store_true", help="recompute rows before the first biased key (A/B)")
     ap.add_argument("--cpu-units", type=int, default=2)
     ap.add_argument("--blas", default="hipblaslt", choices=["hipblas", "hipblaslt"])
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPU) or gloo (rehearsal)")
@@ -124,7 +125,7 @@ def main():
         torch.cuda.synchronize()
         for s in range(args.warmup):
             qi, ids, w, ans = work[s]
-            sweep.ie_question(eng, ids, w, ans)
+            sweep.ie_question(eng, ids, w, ans, skip_prefix=not args.no_prefix_skip)
             torch.cuda.synchronize()
             log(f"[rank {rank}] warmup step {s} done")
         if world > 1:
@@ -137,8 +138,10 @@ def main():
         timed = []
         for s in range(args.steps):
             qi, ids, w, ans = work[args.warmup + s]
-            timed.append(sweep.ie_question(eng, ids, w, ans))
-            flops += sweep.sweep_flops(spec, ids.numel(), ans.numel())
+            timed.append(sweep.ie_question(eng, ids, w, ans, skip_prefix=not args.no_prefix_skip))
+            p0 = int((w.view(-1) != 1).nonzero()[0, 0]) if bool((w != 1).any()) else ids.numel()
+            p0 = 0 if args.no_prefix_skip else p0
+            flops += sweep.sweep_flops(spec, ids.numel(), ans.numel(), p0)
             if rank == 0:
                 log(f"[rank 0] step {s} enqueued ({time.perf_counter() - t_start:.1f}s)")
         local_ie = torch.stack(timed)

@@ -210,13 +210,17 @@ class CrAMEngine:
         return h + self.mlp(x2, lw)
 
     def layer_rows(self, hbuf: torch.Tensor, B: int, T: int, l: int, cos, sin, bias=None, enable=None, W: int = 0,
-                   out_rows: Optional[int] = None, delta: Optional[torch.Tensor] = None):
+                   out_rows: Optional[int] = None, delta: Optional[torch.Tensor] = None, prefix=None):
         """One decoder layer over a ROW buffer: rows [0, B*T) are B sequences of T tokens, rows beyond are
         alignment padding (GEMM M rounded up to the 256-row hipBLASLt/rocBLAS macro tile; padding rows carry
         garbage and are never read back).  The layer input is hbuf [Mp, D], or hbuf + delta when the previous
         layer's MLP output is still pending (the residual add then runs inside this layer's first RMSNorm).
         Returns (h, mlp_out): the layer output is h + mlp_out, left for the next consumer to fuse.
-        out_rows=n returns [B*n, D] pairs (last n rows of every sequence)."""
+        out_rows=n returns [B*n, D] pairs (last n rows of every sequence).
+
+        prefix=(k0, v0, pos): the B sequences are SUFFIXES that start at position p0 = k0.shape[1] of a common
+        prefix whose roped K/V at this layer are k0/v0 [1, p0, Hkv, d] (shared by all B sequences); pos is the
+        int64 [B*T] position of every row.  Attention then runs over p0 + T keys per sequence."""
         sp, lw = self.spec, self.layers[l]
         M = B * T
         if delta is None:
@@ -225,11 +229,22 @@ class CrAMEngine:
             hbuf, x = ops.rmsnorm(delta, lw.ln1, sp.eps, residual=hbuf)
         y = ops.linear(x, lw.wqkv, lw.bqkv)
         yr = y[:M]
-        ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
+        ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T,
+                         pos=None if prefix is None else prefix[2])
         y3 = yr.view(B, T, -1)
         q = y3[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
         k = y3[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
         v = y3[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
+        if prefix is not None:                       # [prefix | suffix] keys per sequence
+            k0, v0, _ = prefix
+            p0 = k0.shape[1]
+            kf = torch.empty((B, p0 + T, sp.num_kv_heads, sp.head_dim), dtype=self.dtype, device=self.device)
+            vf = torch.empty_like(kf)
+            kf[:, :p0] = k0
+            kf[:, p0:] = k
+            vf[:, :p0] = v0
+            vf[:, p0:] = v
+            k, v = kf, vf
         if out_rows is None:
             a = torch.empty((hbuf.shape[0], sp.q_size), dtype=self.dtype, device=self.device)
             ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale, bias=bias,

@@ -75,22 +75,33 @@ def baseline(eng: CrAMEngine, ids: torch.Tensor, n_ans: int, keep: bool = True):
     return eng.rmsnorm(h, eng.norm)[0], qc
 
 
+def first_biased_row(bias: torch.Tensor, W: int) -> int:
+    """p0 = first key position whose credibility bias is not 0.  Query rows before p0 see no biased key, so
+    (causal attention) they are identical in every variant of every layer: the sweep computes rows >= p0
+    only and takes the K/V of rows < p0 from the baseline forward."""
+    nz = torch.nonzero(bias[0, :W] != 0)
+    return int(nz[0, 0]) if nz.numel() else W
+
+
 @torch.no_grad()
 def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tensor, W: int, n_ans: int,
-                   heads: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Final hidden states [H'+1, n, D]: variants 'head heads[i] of layer l re-weighted', then the un-perturbed one."""
+                   heads: Optional[torch.Tensor] = None, p0: int = 0) -> torch.Tensor:
+    """Final hidden states [H'+1, n, D]: variants 'head heads[i] of layer l re-weighted', then the un-perturbed one.
+
+    Rows < p0 (before the first biased key) are taken from the baseline instead of being recomputed per variant."""
     sp = eng.spec
     H = sp.num_heads
     heads = torch.arange(H, device=eng.device) if heads is None else heads
     Hv = heads.numel() + 1                                               # + the un-perturbed variant (last)
-    T = qc.h_in[l].shape[1]
+    T_full = qc.h_in[l].shape[1]
     L = sp.num_layers
     last = l == L - 1
+    p0 = max(0, min(int(p0), T_full - n_ans))                           # the answer rows are always computed
+    T = T_full - p0                                                     # suffix rows per variant
     enable = torch.ones((1, H), dtype=torch.uint8, device=eng.device)
     q, k, v = qc.q[l], qc.k[l], qc.v[l]
     rows = n_ans if last else T
-    if last:
-        q = q[:, -n_ans:]
+    q = q[:, -rows:]
     a_bias = eng.attention(q, k, v, bias, enable, W)                   # [1, rows, Hq, d] every head biased
     a_base = qc.a[l][:, -rows:]
     M = Hv * rows
@@ -106,9 +117,14 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     h, x2 = ops.rmsnorm(ops.linear(abuf, lw.wo), lw.ln2, sp.eps, residual=hin)   # [Mp, D]
     m = eng.mlp(x2, lw)                                                 # layer output h + m, add deferred
     if not last:
-        cos, sin = eng.rope_tables(T)
+        cos, sin = eng.rope_tables(T_full)
+        pos = None
+        if p0 > 0:
+            pos = (torch.arange(T, device=eng.device, dtype=torch.int64) + p0).repeat(Hv)
         for l2 in range(l + 1, L):
-            h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m)
+            pre = None if p0 == 0 else (qc.k[l2][:, :p0], qc.v[l2][:, :p0], pos)
+            h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m,
+                                  prefix=pre)
     rows = Hv * n_ans
     _, y = ops.rmsnorm(m[:rows], eng.norm, sp.eps, residual=h[:rows])   # final norm of h + m
     return y.view(Hv, n_ans, sp.hidden)                                 # [Hv, n, D]
@@ -116,7 +132,7 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
 
 @torch.no_grad()
 def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answer_ids: torch.Tensor,
-                layers=None, round_bf16_logits: bool = False) -> torch.Tensor:
+                layers=None, round_bf16_logits: bool = False, skip_prefix: bool = True) -> torch.Tensor:
     """IE [len(layers), H] (fp32, device) for one question — the value cal_logits returns.
 
     ids [T'] (prompt + answer), weight16 fp16 [T'] (sweep scores), answer_ids [n]
@@ -133,31 +149,38 @@ def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answ
     out = torch.empty((len(layers), sp.num_heads), dtype=torch.float32, device=dev)
     H1 = sp.num_heads + 1
     ans_rep = ans.repeat(H1)
+    p0 = first_biased_row(cb.bias, cb.W) if skip_prefix else 0
     for i, l in enumerate(layers):
-        hv = layer_variants(eng, qc, l, cb.bias, cb.W, n)              # [H+1, n, D]
+        hv = layer_variants(eng, qc, l, cb.bias, cb.W, n, p0=p0)       # [H+1, n, D]
         sums = eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_bf16_logits).view(H1, n).sum(1)
         out[i] = sums[-1] - sums[:-1]                                   # ori - cur
     return out
 
 
-def sweep_flops(spec, T: int, n_ans: int) -> float:
-    """Algorithmic GEMM+attention flops of ie_question (for roofline accounting)."""
+def sweep_flops(spec, T: int, n_ans: int, p0: int = 0) -> float:
+    """Algorithmic GEMM+attention flops of ie_question (for roofline accounting); p0 = skipped prefix rows."""
     L, H, d, D = spec.num_layers, spec.num_heads, spec.head_dim, spec.hidden
-    attn = lambda tq, s: 4.0 * d * spec.num_heads * tq * (s + 1) / 2.0 if tq == s else 4.0 * d * spec.num_heads * tq * s
+
+    def attn(tq, s):   # tq queries at positions s-tq .. s-1, causal
+        vis = tq * (s - tq) + tq * (tq + 1) / 2.0
+        return 4.0 * d * spec.num_heads * vis
+
     lay = lambda t: spec.layer_flops(t)
-    f = 0.0
-    # baseline: L-1 full layers + last layer (qkv over T, rest over n)
     qkv_frac = (spec.q_size + 2 * spec.kv_size) * D / ((spec.q_size + 2 * spec.kv_size) * D + spec.q_size * D
                                                       + 3 * D * spec.intermediate)
+    p0 = max(0, min(p0, T - n_ans))
+    Ts = T - p0
+    f = 0.0
+    # baseline: L-1 full layers + last layer (qkv over T, rest over n)
     f += (L - 1) * (lay(T) + attn(T, T)) + qkv_frac * lay(T) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T)
     for l in range(L):
         last = l == L - 1
-        rows = n_ans if last else T
+        rows = n_ans if last else Ts
         f += attn(rows, T)                                              # all-heads biased attention
         f += (H + 1) * (1 - qkv_frac) * lay(rows)                       # o_proj + MLP of layer l, H+1 variants
         for l2 in range(l + 1, L):
             if l2 == L - 1:
-                f += (H + 1) * (qkv_frac * lay(T) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T))
+                f += (H + 1) * (qkv_frac * lay(Ts) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T))
             else:
-                f += (H + 1) * (lay(T) + attn(T, T))
+                f += (H + 1) * (lay(Ts) + attn(Ts, T))
     return f

@@ -232,3 +232,22 @@ def test_cpu_baseline_model_matches_engine():
     assert (got - ref).abs().max() < 0.1 and (got - ref).abs().mean() < 0.02
     r = cpu_baseline.time_ie_units(model, ids, w, torch.tensor([5, 6]), [(0, 1), (1, 2)])
     assert r["units"] == 2 and r["units_per_s"] > 0 and all(np.isfinite(r["ie"]))
+
+
+def test_sweep_prefix_skip_is_exact(tiny, nq):
+    """Rows before the first biased key are identical in every variant: computing only the suffix (K/V of
+    the prefix from the baseline forward) gives the same IE as recomputing every row."""
+    path, tok, model = tiny["llama3"]
+    eng = CrAMEngine.from_hf(model)
+    ids, w = _question(tok, path, nq[0])
+    ans = tok([nq[0]["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
+    from cram_amd.bias import CredibilityBias
+    p0 = sweep.first_biased_row(CredibilityBias.build([w], {}, 1, 1, "cpu").bias, w.shape[-1])
+    assert 0 < p0 < ids.shape[1] - ans.numel()
+    with cpu_ops.patched_ops():
+        a = sweep.ie_question(eng, ids[0], w[0], ans, skip_prefix=True)
+        b = sweep.ie_question(eng, ids[0], w[0], ans, skip_prefix=False)
+    assert torch.equal(a, b)
+    T = ids.shape[1]
+    assert sweep.sweep_flops(eng.spec, T, ans.numel(), p0) < sweep.sweep_flops(eng.spec, T, ans.numel())
+
