@@ -72,8 +72,18 @@ def register() -> str:
 
 
 def attention_modules(model):
-    for l, layer in enumerate(model.model.layers):
-        yield l, layer.self_attn
+    """(layer index, attention module) of a decoder-only transformers model: `model.layers.{l}.self_attn`
+    (Llama / Qwen2 / Mistral families, re_weighting.py:120) or `transformer.h.{l}.attn` (GPT-2, which the
+    reference's hook path cannot address)."""
+    base = model.base_model
+    if hasattr(base, "layers"):
+        for l, layer in enumerate(base.layers):
+            yield l, layer.self_attn
+    elif hasattr(base, "h"):
+        for l, blk in enumerate(base.h):
+            yield l, blk.attn
+    else:
+        raise NotImplementedError(f"no known attention-module layout for {type(model).__name__}")
 
 
 @contextlib.contextmanager

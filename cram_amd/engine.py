@@ -106,6 +106,13 @@ class CrAMEngine:
         self.scale = spec.head_dim ** -0.5
 
     # ------------------------------------------------------------------ construction
+    SUPPORTED = ("llama", "qwen2")
+
+    @staticmethod
+    def supports(model) -> bool:
+        """The engine re-implements the Llama / Qwen2 decoder (RMSNorm, RoPE, SwiGLU, GQA)."""
+        return getattr(model.config, "model_type", "") in CrAMEngine.SUPPORTED
+
     @staticmethod
     def from_hf(model) -> "CrAMEngine":
         """Share the transformers model's weights (q/k/v and gate/up are concatenated once)."""

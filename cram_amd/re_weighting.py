@@ -48,6 +48,9 @@ class Re_Weighting_Strategy:
     @property
     def engine(self) -> CrAMEngine:
         if self._engine is None:
+            if not CrAMEngine.supports(self.model):
+                raise NotImplementedError(f"the batched engine supports {CrAMEngine.SUPPORTED} models, not "
+                                          f"{self.model.config.model_type!r}")
             self._engine = CrAMEngine.from_hf(self.model)
         return self._engine
 
@@ -189,8 +192,39 @@ class Find_Best_Heads(Re_Weighting_Strategy):
         L, H = self.model_num_hidden_layers, self.model_num_attention_heads
         if ans.numel() == 0:   # the reference sums an empty selection: IE == 0 everywhere
             return torch.zeros((L, H), dtype=torch.float32, device=self.device)
+        if not CrAMEngine.supports(self.model):
+            return self._ie_per_head(model_inputs["input_ids"], w, ans, round_bf16_logits)
         return _sweep.ie_question(self.engine, model_inputs["input_ids"][0], w[0].cpu(), ans,
                                   round_bf16_logits=round_bf16_logits)
+
+    @torch.no_grad()
+    def _ie_per_head(self, ids: torch.Tensor, w16: torch.Tensor, ans: torch.Tensor,
+                     round_bf16_logits: bool) -> torch.Tensor:
+        """The reference algorithm itself (re_weighting.py:157-175: one un-hooked forward, then one forward per
+        (layer, head) with only that head re-weighted) on the transformers model with the cram_hip kernels, for
+        architectures the batched engine does not implement (GPT-2).  Answer logits in fp32 like the sweep."""
+        L, H = self.model_num_hidden_layers, self.model_num_attention_heads
+        n = int(ans.numel())
+        ans_d = ans.to(self.device, torch.int32)
+        w_lm = self.model.get_output_embeddings().weight
+
+        def total(cb):
+            with _attn.reweighting(self.model, cb):
+                hid = self.model.base_model(input_ids=ids).last_hidden_state[0, -n:]
+            return self._answer_logits(hid, w_lm, ans_d, round_bf16_logits).sum()
+
+        ori = total(None)
+        out = torch.empty((L, H), dtype=torch.float32, device=self.device)
+        for l in range(L):
+            for h in range(H):
+                out[l, h] = ori - total(self._bias(w16, {l: [h]}))
+        return out
+
+    @staticmethod
+    def _answer_logits(hidden, w_lm, ids, round_bf16):
+        from . import ops
+        return ops.answer_logits(hidden.to(torch.bfloat16).contiguous(), w_lm.to(torch.bfloat16), ids,
+                                 round_bf16=round_bf16)
 
     @torch.no_grad()
     def cal_logits_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],

@@ -155,13 +155,34 @@ def _pre_hook(module, args, kwargs, *, num_heads, lw, head_idx):
     return args, kwargs
 
 
+def _pre_hook_gpt2(module, args, kwargs, *, num_heads, lw, head_idx):
+    """GPT-2 adapter: GPT2Attention gets hidden_states POSITIONALLY and lives at
+    transformer.h.{l}.attn, so the reference hook cannot run on it; the same mask edit, with S from
+    position_ids (cache_position, or T for a cache-less forward, when absent)."""
+    hs = args[0] if args else kwargs["hidden_states"]
+    T = hs.shape[1]
+    pos = kwargs.get("position_ids")
+    if pos is None:
+        cp = kwargs.get("cache_position")
+        pos = cp.view(1, -1) if cp is not None else torch.arange(T).view(1, -1)
+    kwargs["attention_mask"] = edit_attention_mask(num_heads, hs, kwargs.get("attention_mask"), pos, lw, head_idx)
+    return args, kwargs
+
+
+def attention_module_name(model, layer: int) -> str:
+    """`model.layers.{l}.self_attn` (re_weighting.py:120) or `transformer.h.{l}.attn` (GPT-2)."""
+    return (f"transformer.h.{layer}.attn" if getattr(model.config, "model_type", "") == "gpt2"
+            else f"model.layers.{layer}.self_attn")
+
+
 def register_hooks(model, layers_to_heads: dict, lw: torch.Tensor) -> list:
     """re_weighting.py:118-124 / :163-168: one forward-pre-hook per selected layer."""
     H = model.config.num_attention_heads
+    hook = _pre_hook_gpt2 if getattr(model.config, "model_type", "") == "gpt2" else _pre_hook
     handles = []
     for layer, heads in layers_to_heads.items():
-        mod = model.get_submodule(f"model.layers.{int(layer)}.self_attn")
-        handles.append(mod.register_forward_pre_hook(partial(_pre_hook, num_heads=H, lw=lw, head_idx=list(heads)),
+        mod = model.get_submodule(attention_module_name(model, int(layer)))
+        handles.append(mod.register_forward_pre_hook(partial(hook, num_heads=H, lw=lw, head_idx=list(heads)),
                                                      with_kwargs=True))
     return handles
 

@@ -237,3 +237,48 @@ def test_cal_logits_batch_equals_per_question(fbh, nq):
     for i, r in enumerate(recs):
         one = obj.cal_logits_tensor(args[0][i], args[1][i], [0, 1, 1, 1, 1], "", args[3][i])
         assert torch.equal(batch[i], one)
+
+
+def test_gpt2_config1_family_on_gpu(tmp_path_factory, nq, gpu_device):
+    """SURVEY §8d config 1 family (GPT-2: MHA, head_dim 64, transformer.h.{l}.attn) through the drop-in on the
+    HIP kernels: re-weighted answer log-probs, the IE grid (per-head forwards: the batched engine is Llama /
+    Qwen2 only) and a greedy decode, against the oracle's GPT-2 hook adapter (the reference's hook cannot
+    run on GPT-2, so this parity is oracle-pinned only).  Same noise-floor bars as the other families."""
+    from transformers import AutoModelForCausalLM
+    from cram_amd.re_weighting import Find_Best_Heads, Re_Weighting_Strategy
+    from oracle import hook_ref
+    root = str(tmp_path_factory.mktemp("gpt2"))
+    path, path32 = tm.save_model("gpt2", root), tm.save_model("gpt2", root, fp32=True)
+    m16 = AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval()
+    m32 = AutoModelForCausalLM.from_pretrained(path32, dtype="auto").eval()
+    heads = {"0": [1], "2": [0, 3]}
+    rw = Re_Weighting_Strategy(model_name=path, layers_to_be_modified=heads)
+    for rec in nq[:3]:
+        paras = rec["ori_fake"] + rec["reranked_dense_ctxs"]
+        lp = rw.answer_logprobs(question=rec["question"], paras=paras, scores=[0.1, 1, 1, 1, 1],
+                                answer=rec["wrong_answer"]).cpu().numpy()
+        enc, w = rw.decode_with_special_attention(question=rec["question"], paras=paras, scores=[0.1, 1, 1, 1, 1],
+                                                  answer=rec["wrong_answer"])
+        ids, lw = enc["input_ids"].cpu(), hook_ref.log_weight(w.cpu())
+        hi = {int(k): v for k, v in heads.items()}
+        truth = hook_ref.answer_logprobs(m32, ids, lw, hi, lp.size).numpy()
+        ref = hook_ref.answer_logprobs(m16, ids, lw, hi, lp.size).numpy()
+        assert np.abs(lp - truth).max() <= 2.5 * np.abs(ref - truth).max() + 0.01
+    out = rw.run_RAG_with_attention_weighting(question=nq[0]["question"], paras=nq[0]["ori_fake"][:1], scores=[0.1])
+    assert isinstance(out, tuple) and isinstance(out[1], str)
+
+    fbh = Find_Best_Heads(model_name=path)
+    rec = nq[0]
+    paras = rec["ori_fake"] + rec["reranked_dense_ctxs"]
+    ie = np.array(fbh.cal_logits(question=rec["question"], paras=paras, scores=[0, 1, 1, 1, 1],
+                                 wrong_answer=rec["wrong_answer"]))
+    enc, w = fbh.decode_with_special_attention(question=rec["question"], paras=paras, scores=[0, 1, 1, 1, 1],
+                                               answer=rec["wrong_answer"])
+    ids, lw, ans = enc["input_ids"].cpu(), hook_ref.log_weight(w.cpu()), fbh.answer_ids(rec["wrong_answer"])
+    truth = hook_ref.ie_grid(m32, ids, lw, ans)
+    h = m16.lm_head.register_forward_hook(lambda mod, a, o: torch.nn.functional.linear(a[0].float(), mod.weight.float()))
+    try:
+        ref = hook_ref.ie_grid(m16, ids, lw, ans)
+    finally:
+        h.remove()
+    ie_tolerance_check(ie, ref, truth)

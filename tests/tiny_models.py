@@ -15,8 +15,10 @@ import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TOK_DIR = {"llama3": os.path.join(REPO, "data", "tok_llama3"), "qwen2": os.path.join(REPO, "data", "tok_qwen")}
-DIR_NAME = {"llama3": "Llama-3-tiny", "qwen2": "Qwen2-tiny"}   # names select the reference's chat branch
+TOK_DIR = {"llama3": os.path.join(REPO, "data", "tok_llama3"), "qwen2": os.path.join(REPO, "data", "tok_qwen"),
+           "gpt2": os.path.join(REPO, "data", "tok_llama3")}
+# names select the reference's chat branch; "gpt2-tiny" matches neither, i.e. the raw-template branch
+DIR_NAME = {"llama3": "Llama-3-tiny", "qwen2": "Qwen2-tiny", "gpt2": "gpt2-tiny"}
 
 SPECS = {
     "llama3": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=4, num_attention_heads=4,
@@ -25,6 +27,8 @@ SPECS = {
     "qwen2": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=3, num_attention_heads=2,
                   num_key_value_heads=1, rope_theta=1000000.0, rms_norm_eps=1e-6,
                   max_position_embeddings=4096, tie_word_embeddings=False),
+    # GPT-2 architecture (config 1's family): MHA, head_dim 64, learned positions, LayerNorm, GELU
+    "gpt2": dict(n_embd=256, n_inner=512, n_layer=3, n_head=4, n_positions=4096),
 }
 SEED = 20250404
 LIN_STD = 0.08
@@ -42,10 +46,12 @@ def tokenizer(kind: str):
 
 
 def config(kind: str):
-    from transformers import LlamaConfig, Qwen2Config
+    from transformers import GPT2Config, LlamaConfig, Qwen2Config
     tok = tokenizer(kind)
     spec = dict(SPECS[kind])
-    if kind == "llama3":
+    if kind == "gpt2":
+        cfg = GPT2Config(vocab_size=len(tok), bos_token_id=tok.bos_token_id, eos_token_id=tok.eos_token_id, **spec)
+    elif kind == "llama3":
         cfg = LlamaConfig(vocab_size=len(tok), bos_token_id=tok.bos_token_id, eos_token_id=tok.eos_token_id,
                           **spec)
     else:
@@ -61,8 +67,12 @@ def build_model(kind: str, attn_implementation: str = "sdpa"):
     model = AutoModelForCausalLM.from_config(cfg, attn_implementation=attn_implementation, dtype=torch.bfloat16)
     sd = {}
     for name, p in model.state_dict().items():
-        if name.endswith("norm.weight") or "layernorm" in name:
+        if name.endswith("norm.weight") or "layernorm" in name or (".ln_" in name and name.endswith("weight")):
             sd[name] = _draw(name, tuple(p.shape), 0.1, 1.0)
+        elif name.endswith(".attn.bias") or name.endswith(".masked_bias"):   # GPT-2 causal buffers, not weights
+            sd[name] = p
+        elif name.endswith("wte.weight") or name.endswith("wpe.weight"):        # GPT-2: tied lm_head
+            sd[name] = _draw(name, tuple(p.shape), 0.3 if name.endswith("wte.weight") else 0.1)
         elif name.endswith("embed_tokens.weight"):
             sd[name] = _draw(name, tuple(p.shape), 1.0)
         elif name.endswith(".bias"):
