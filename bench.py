@@ -5,7 +5,8 @@ Default (config 3 + 2): one step = the full Find_Best_Heads IE sweep (32 layers 
 no data-path collective), plus one RCCL all-gather of the IE grids at the end of
 the timed region.  The primary `value` is heads/s over all ranks; the batched
 reweighted decode (questions/s, config 2) is reported next to it as `decode`.
-Other BASELINE configs:  --config 2 (decode as the primary value),
+Other BASELINE configs:  --config 1 (GPT-2-small, 8 NQ questions x 5 docs, the reference's batch-1 hooked
+decode shape: drop-in on the HIP kernels vs the CPU hook path), --config 2 (decode as the primary value),
 --config 4 (Qwen2-7B, TriviaQA, ideal scores, all heads, decode),
 --config 5 (Llama-3-8B, 20 retrieved docs ~8k tokens, decode).
 
@@ -64,7 +65,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--decode-batch", type=int, default=64)
     ap.add_argument("--decode-tokens", type=int, default=16)
     ap.add_argument("--no-decode", action="store_true")
@@ -82,6 +83,8 @@ def main():
     from cram_amd import ops, scores, spans, sweep
     from cram_amd.engine import CrAMEngine, ModelSpec, configure_blas
 
+    if args.config == 1:
+        return run_config1(args)
     rank, world, local = cdist.init(args.dist_backend)
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
@@ -294,6 +297,88 @@ def main():
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+
+
+def run_config1(args):
+    """BASELINE config 1: GPT-2-small (12 x 12 heads, d 64, random init), the first 8 NQ questions x 5 passages,
+    ideal scores [0.1, 1, 1, 1, 1], all heads re-weighted (layers_to_be_modified = {}), greedy decode of a fixed
+    32 tokens at batch 1 exactly as run_RAG_with_attention_weighting runs it (transformers generate), with the
+    cram_hip kernels on 1 GPU; next to it the same decode through the dense-mask hook on the host cores."""
+    import torch
+    from transformers import AutoTokenizer, GPT2Config, GPT2LMHeadModel
+    from cram_amd import attention as A
+    from cram_amd import spans
+    from cram_amd.bias import CredibilityBias, all_heads
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    cfg = GPT2Config(n_layer=12, n_head=12, n_embd=768, n_positions=1024, vocab_size=50257)
+    A.register()
+    cpu_model = GPT2LMHeadModel(cfg).to(torch.bfloat16).eval()
+    import copy
+    gpu_model = GPT2LMHeadModel(copy.deepcopy(cfg)).to(torch.bfloat16).eval()     # own config: own attention impl
+    gpu_model.load_state_dict(cpu_model.state_dict())
+    gpu_model.set_attn_implementation(A.IMPL_NAME)
+    gpu_model = gpu_model.to(dev)
+    tok = AutoTokenizer.from_pretrained(os.path.join(REPO, "data", "tok_llama3"))
+    name = "gpt2-small"                                  # no chat branch: raw template (re_weighting.py:96-97)
+    data = load_dataset("nq")[:8]
+    L, H = cfg.n_layer, cfg.n_head
+    heads = all_heads(L, H)
+    prompts = []
+    for rec in data:
+        _, enc, w, _ = spans.encode(tok, name, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
+                                    [0.1, 1, 1, 1, 1], "")
+        prompts.append((enc["input_ids"], w))
+    gen = dict(do_sample=False, max_new_tokens=32, min_new_tokens=32, pad_token_id=0)
+
+    def run_gpu():
+        outs = []
+        for ids, w in prompts:
+            cb = CredibilityBias.build([w], heads, L, H, dev)
+            idd = ids.to(dev)
+            with A.reweighting(gpu_model, cb), torch.no_grad():
+                outs.append(gpu_model.generate(input_ids=idd, attention_mask=torch.ones_like(idd), **gen))
+        return outs
+
+    run_gpu()                                             # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(max(1, args.steps)):
+        run_gpu()
+    torch.cuda.synchronize()
+    gpu_s = (time.perf_counter() - t0) / max(1, args.steps)
+    value = len(prompts) / gpu_s
+    log(f"[config 1] GPU drop-in: {value:.2f} questions/s ({gpu_s:.2f} s for 8 questions)")
+    cpu = None
+    if not args.no_cpu_baseline:
+        from oracle import cpu_baseline, hook_ref
+        torch.set_num_threads(cpu_baseline.cores())
+        n_cpu = 2                                         # bounded sample: 2 of the 8 questions
+        t0 = time.perf_counter()
+        for ids, w in prompts[:n_cpu]:
+            hs = hook_ref.register_hooks(cpu_model, heads, hook_ref.log_weight(w))
+            try:
+                with torch.no_grad():
+                    cpu_model.generate(input_ids=ids, attention_mask=torch.ones_like(ids), **gen)
+            finally:
+                for h in hs:
+                    h.remove()
+        cs = time.perf_counter() - t0
+        cpu = {"value": n_cpu / cs, "unit": "questions/s", "cores": cpu_baseline.cores(), "kind": "port",
+               "sample": f"{n_cpu} of the 8 questions, 32 greedy tokens each through transformers + the restated "
+                         f"dense-mask hook on every layer (GPT-2 adapter), bf16 CPU, {cs:.1f}s"}
+        log(f"[config 1] CPU hook path: {cpu['value']:.3f} questions/s on {cpu['cores']} cores")
+    T_mean = sum(ids.shape[1] for ids, _ in prompts) / len(prompts)
+    print(json.dumps({
+        "metric": METRIC + " [config 1: GPT-2-small reweighted decode]", "value": round(value, 3),
+        "unit": "questions/s", "n_gpus": 1, "steps": args.steps, "warmup": 1, "ms_per_step": round(gpu_s * 1e3, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic: random-init GPT-2-small weights; first 8 rebuilt NQ prompts (raw template)",
+        "config": {"workload": "GPT-2-small, 8 NQ questions x 5 retrieved docs, batch-1 hooked-decode shape, all "
+                               "heads re-weighted, 32 new tokens", "model": "gpt2-small",
+                   "mean_prompt_tokens": round(T_mean, 1), "parallelism": "single GPU, batch 1"},
+        "roofline": None, "cpu_baseline": cpu,
+        "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None}), flush=True)
 
 
 if __name__ == "__main__":
