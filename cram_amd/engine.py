@@ -202,13 +202,11 @@ class CrAMEngine:
                                 bias=bias, enable=enable, W=W)
 
     def layer(self, h: torch.Tensor, l: int, cos, sin, bias=None, enable=None, W: int = 0,
-              out_rows: Optional[int] = None, kv_out=None) -> torch.Tensor:
+              out_rows: Optional[int] = None) -> torch.Tensor:
         """One decoder layer over h [B, T, D].  out_rows=n computes attention/MLP for the last n rows only."""
         lw = self.layers[l]
         x = self.rmsnorm(h, lw.ln1)
         q, k, v = self.qkv(x, lw, cos, sin)
-        if kv_out is not None:
-            kv_out(l, k, v)
         if out_rows is not None:
             q = q[:, -out_rows:]
             h = h[:, -out_rows:]
@@ -267,19 +265,17 @@ class CrAMEngine:
         return h2, self.mlp(x2, lw)
 
     @torch.no_grad()
-    def forward_hidden(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None, out_rows: Optional[int] = None,
-                       kv_out=None, layer_hook=None) -> torch.Tensor:
+    def forward_hidden(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None,
+                       out_rows: Optional[int] = None) -> torch.Tensor:
         """ids [B, T] -> final-norm hidden states [B, T or out_rows, D]."""
         B, T = ids.shape
         cos, sin = self.rope_tables(T)
         h = self.embed[ids]
         L = self.spec.num_layers
         for l in range(L):
-            if layer_hook is not None:
-                layer_hook(l, h)
             en = cb.enable[l] if cb is not None else None
             h = self.layer(h, l, cos, sin, cb.bias if cb is not None else None, en, cb.W if cb is not None else 0,
-                           out_rows=out_rows if l == L - 1 else None, kv_out=kv_out)
+                           out_rows=out_rows if l == L - 1 else None)
         return self.rmsnorm(h, self.norm)
 
     @torch.no_grad()
@@ -308,16 +304,12 @@ class CrAMEngine:
         if use_graph and steps > 0:
             sess.capture()
         eos = torch.tensor(list(eos_ids) or [-1], device=self.device)
-        done_at = None
         for t in range(steps):
             sess.step(use_graph)
+            # every 8 steps: stop once every row has produced an EOS (one host sync per check)
             if stop_on_eos and eos_ids and (t % 8 == 7 or t == steps - 1):
-                gen = sess.generated()
-                hit = torch.isin(gen, eos).any(1)
-                if bool(hit.all()):
-                    done_at = t
+                if bool(torch.isin(sess.generated(), eos).any(1).all()):
                     break
-        del done_at
         out = []
         gen = sess.generated().cpu().tolist()
         for row in gen:
@@ -386,8 +378,12 @@ class DecodeSession:
         h[:total] = eng.embed[torch.cat(self.prompts)]
         if Mp > total:
             h[total:].zero_()
+        m = None                                     # pending MLP output: layer output = h + m (add fused below)
         for l, lw in enumerate(eng.layers):
-            x = ops.rmsnorm(h, lw.ln1, sp.eps)
+            if m is None:
+                x = ops.rmsnorm(h, lw.ln1, sp.eps)
+            else:
+                h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
             y = ops.linear(x, lw.wqkv, lw.bqkv)
             yr = y[:total]
             ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, self.cos, self.sin, T=1, pos=pos)
@@ -403,24 +399,10 @@ class DecodeSession:
                                     enable=self.cb.enable[l], W=self.cb.W,
                                     out=a[:total].view(total, sp.num_heads, sp.head_dim))
             h, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
-            h = h + eng.mlp(x2, lw)
-        hn = eng.rmsnorm(h[cu[1:].long() - 1], eng.norm)
+            m = eng.mlp(x2, lw)
+        last = cu[1:].long() - 1
+        _, hn = ops.rmsnorm(m[last], eng.norm, sp.eps, residual=h[last])
         self.tokens.copy_(self._pick(ops.linear(hn, eng.lm_head)))
-        self.out[:, 0] = self.tokens
-        self.t.fill_(1)
-
-    def prefill_one_by_one(self):
-        eng = self.eng
-        for b, ids in enumerate(self.prompts):
-            T = ids.numel()
-
-            def kv_out(l, k, v, b=b, T=T):
-                self.k_cache[l, b, :, :T] = k[0].transpose(0, 1)
-                self.v_cache[l, b, :, :T] = v[0].transpose(0, 1)
-
-            sub = CredibilityBias(self.cb.bias[b:b + 1], self.cb.enable[:, b:b + 1], self.cb.W)
-            h = eng.forward_hidden(ids[None], sub, out_rows=1, kv_out=kv_out)
-            self.tokens[b] = self._pick(ops.linear(h[0, -1], eng.lm_head))
         self.out[:, 0] = self.tokens
         self.t.fill_(1)
 
