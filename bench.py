@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--decode-batch", type=int, default=64)
+    ap.add_argument("--decode-batch", type=int, default=256)
     ap.add_argument("--decode-tokens", type=int, default=16)
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--scores", default="ideal", choices=["ideal", "gpt"],
