@@ -262,17 +262,15 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
           for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[kb][e]);
         mx *= p.scale_log2;
       } else if (!need_mask) {                                   // biased head, interior tile
+        // raw scores stay in sacc: the exponent below is fma(s, c, b - m), which for b == 0 is exactly
+        // the plain path's fma(s, c, -m) (a zero bias is bit-identical to no bias)
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + kb * 32 + 8 * g + 4 * hh);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float s = __builtin_fmaf(sacc[kb][4 * g + e], p.scale_log2, bv[e]);
-              sacc[kb][4 * g + e] = s;
-              mx = fmaxf(mx, s);
-            }
+            for (int e = 0; e < 4; ++e) mx = fmaxf(mx, __builtin_fmaf(sacc[kb][4 * g + e], p.scale_log2, bv[e]));
           }
         }
       } else {                                                   // diagonal / ragged tile
@@ -298,16 +296,31 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       const float mnew = fmaxf(m, mx);
       const float muse = (mnew == kNegInf) ? 0.f : mnew;
       const float alpha = fast_exp2(m - muse);
-      const float sc = plain ? p.scale_log2 : 1.f;
       float rs = 0.f;
+      if (!plain && !need_mask) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float pe = fast_exp2(__builtin_fmaf(sacc[kb][e], sc, -muse));
-          sacc[kb][e] = pe;
-          rs += pe;
-        }
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + kb * 32 + 8 * g + 4 * hh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float pe = fast_exp2(__builtin_fmaf(sacc[kb][4 * g + e], p.scale_log2, bv[e] - muse));
+              sacc[kb][4 * g + e] = pe;
+              rs += pe;
+            }
+          }
+      } else {
+        const float sc = plain ? p.scale_log2 : 1.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float pe = fast_exp2(__builtin_fmaf(sacc[kb][e], sc, -muse));
+            sacc[kb][e] = pe;
+            rs += pe;
+          }
+      }
       rs = half_sum(rs);
       l = l * alpha + rs;
       m = mnew;

@@ -245,3 +245,118 @@ def test_prefill_varlen_matches_oracle(gpu_device, lens, Hq, Hkv):
                                   bias=bias.to(dev), enable=enable.to(dev), W=W)
     torch.cuda.synchronize()
     _check(out, ref)
+
+
+def _rows_ref(q, k, v, bias, enable, W, scale, b, h, rows, G):
+    """float64 reference for a few query rows of one (batch, head): causal over keys <= row (q_pos0 = 0),
+    bias[b, j] added for j < W when the head is enabled (the hook's semantics, re_weighting.py:57-59)."""
+    out = []
+    kk = k[b, h // G].double()
+    vv = v[b, h // G].double()
+    for i in rows:
+        s = (kk[:i + 1] @ q[b, h, i].double()) * scale
+        if bias is not None and enable[b, h]:
+            jb = min(i + 1, W)
+            s[:jb] += bias[b, :jb].double()
+        p = torch.softmax(s, 0)
+        out.append(p @ vv[:i + 1])
+    return torch.stack(out)
+
+
+@pytest.mark.parametrize("B,T", [(33, 962), (1, 8300)])
+def test_prefill_full_size_properties(gpu_device, B, T):
+    """BASELINE sizes (the IE sweep's 33-variant batch at T' = 962; config 5's 8k prompt), Llama-3 GQA 32/8.
+    Size-independent properties, bit-exact: zero bias on every head == no bias; each batch element equals
+    its own single-sequence launch; two q-heads of one GQA group with equal queries give equal outputs.
+    Sampled rows (first, tile edges, last) of biased heads with -inf and 0.1 spans vs float64 (the usual
+    bf16 tolerance)."""
+    from cram_amd import ops
+    dev = gpu_device
+    Hq, Hkv, d = 32, 8, 128
+    G = Hq // Hkv
+    g = torch.Generator(device=dev).manual_seed(B * 7 + T)
+    q = torch.randn(B, T, Hq, d, generator=g, device=dev).to(torch.bfloat16).transpose(1, 2)
+    with torch.no_grad():
+        q[:, 5] = q[:, 4]                                           # heads 4, 5: same kv head (G = 4)
+    k = torch.randn(B, Hkv, T, d, generator=g, device=dev).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, T, d, generator=g, device=dev).to(torch.bfloat16)
+    scale = d ** -0.5
+    plain = ops.attn_prefill(q, k, v, scale=scale)
+    zero = ops.attn_prefill(q, k, v, scale=scale, bias=torch.zeros(B, T, device=dev),
+                            enable=torch.ones(B, Hq, dtype=torch.uint8, device=dev), W=T)
+    assert torch.equal(plain, zero)
+    assert torch.equal(plain[:, :, 4], plain[:, :, 5])
+    for b in sorted({0, B // 2, B - 1}):
+        one = ops.attn_prefill(q[b:b + 1], k[b:b + 1], v[b:b + 1], scale=scale)
+        assert torch.equal(one[0], plain[b])
+    W = T - 5
+    w = torch.ones(B, W, dtype=torch.float16)
+    w[:, 30:200] = 0.0                                              # -inf span (score 0)
+    w[:, 400:700] = 0.1                                             # log 0.1 span
+    bias = hook_ref.log_weight(w).to(torch.bfloat16).float()
+    enable = torch.zeros(B, Hq, dtype=torch.uint8)
+    enable[:, ::3] = 1
+    out = ops.attn_prefill(q, k, v, scale=scale, bias=bias.to(dev), enable=enable.to(dev), W=W)
+    torch.cuda.synchronize()
+    rows = [0, 1, 63, 64, 250, T // 2, T - 1]
+    qc, kc, vc, oc = q.cpu(), k.cpu(), v.cpu(), out.cpu()
+    for b in sorted({0, B - 1}):
+        for h in (0, 1, 3, Hq - 1):
+            ref = _rows_ref(qc, kc, vc, bias, enable, W, scale, b, h, rows, G)
+            _check(oc[b, rows, h], ref)
+
+
+def test_varlen_full_size_equals_dense(gpu_device):
+    """Config 2's packed prefill shape (64 prompts of 700-1100 tokens): every packed sequence equals its own
+    dense single-sequence launch bit for bit (same tiles, same arithmetic)."""
+    from cram_amd import ops
+    dev = gpu_device
+    Hq, Hkv, d = 32, 8, 128
+    g = torch.Generator(device=dev).manual_seed(11)
+    lens = torch.randint(700, 1101, (64,), generator=torch.Generator().manual_seed(3)).tolist()
+    total = sum(lens)
+    qkv = torch.randn(total, (Hq + 2 * Hkv) * d, generator=g, device=dev).to(torch.bfloat16)
+    q = qkv[:, :Hq * d].view(total, Hq, d)
+    k = qkv[:, Hq * d:(Hq + Hkv) * d].view(total, Hkv, d)
+    v = qkv[:, (Hq + Hkv) * d:].view(total, Hkv, d)
+    cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device=dev)
+    out = ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=d ** -0.5)
+    for i in (0, 17, 63):
+        a, n = int(cu[i]), lens[i]
+        one = ops.attn_prefill(q[a:a + n].transpose(0, 1)[None], k[a:a + n].transpose(0, 1)[None],
+                               v[a:a + n].transpose(0, 1)[None], scale=d ** -0.5)
+        assert torch.equal(one[0], out[a:a + n])
+
+
+def test_decode_full_size_sampled(gpu_device):
+    """Config 2's decode step (256 sequences, 700-1100 cached keys, split-S by the engine's rule, top-half
+    heads biased with a -inf and a 0.1 span) on sampled sequences vs float64."""
+    from cram_amd import ops
+    dev = gpu_device
+    B, Hq, Hkv, d, S_max = 256, 32, 8, 128, 1152
+    g = torch.Generator(device=dev).manual_seed(5)
+    q = torch.randn(B, Hq, d, generator=g, device=dev).to(torch.bfloat16)
+    k = torch.randn(B, Hkv, S_max, d, generator=g, device=dev).to(torch.bfloat16)
+    v = torch.randn(B, Hkv, S_max, d, generator=g, device=dev).to(torch.bfloat16)
+    lens = torch.randint(700, 1101, (B,), generator=torch.Generator().manual_seed(9))
+    W = 690
+    w = torch.ones(B, W, dtype=torch.float16)
+    w[:, 20:150] = 0.0
+    w[:, 300:500] = 0.1
+    bias = hook_ref.log_weight(w).to(torch.bfloat16).float()
+    enable = torch.zeros(B, Hq, dtype=torch.uint8)
+    enable[:, :16] = 1
+    splits = 2
+    ws = torch.empty(ops.decode_workspace_bytes(B, Hq, d, splits), dtype=torch.uint8, device=dev)
+    out = ops.attn_decode(q, k, v, scale=d ** -0.5, seq_lens=lens.to(torch.int32).to(dev), bias=bias.to(dev),
+                          enable=enable.to(dev), W=W, num_splits=splits, workspace=ws).cpu()
+    qc, kc, vc = q.cpu(), k.cpu(), v.cpu()
+    for b in (0, 101, 255):
+        L = int(lens[b])
+        for h in (0, 15, 16, 31):
+            kk, vv = kc[b, h // 4, :L].double(), vc[b, h // 4, :L].double()
+            s = (kk @ qc[b, h].double()) * d ** -0.5
+            if enable[b, h]:
+                s[:W] += bias[b].double()
+            ref = torch.softmax(s, 0) @ vv
+            _check(out[b, h][None], ref[None])
