@@ -33,6 +33,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+typedef __attribute__((address_space(3))) void lds_void;
 
 // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): wait for vector-memory loads only (gfx9 encoding)
 constexpr int kWaitVmcnt0 = 0x0F70;
@@ -168,30 +169,44 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   // K/V/bias staging through buffer descriptors: per-thread byte offsets are loop invariant, the
   // per-tile base and the valid extent live in scalar registers, and the descriptor's range check
   // returns zeros past key S (no per-load VALU address math, no bounds compares).
-  uint32_t koff[C::CPT], voff[C::CPT], ldsk[C::CPT], ldsv[C::CPT];
+  // K/V staging by LDS-DMA (buffer_load ... lds): no VGPR staging, no ds_write.  One wave-instruction
+  // writes 1 KiB of the padded (K | V) image of a tile = 64 lanes x 16 B; lane p of chunk c fetches
+  // the 16 bytes that belong at image offset c*1024 + 16p (a pad slot gets an out-of-range offset, so
+  // the descriptor's range check writes zeros there, as it does for rows past key S).
+  constexpr int KCH = C::K_BYTES / 1024, NCH = KCH + C::V_BYTES / 1024;
+  static_assert(C::K_BYTES % 1024 == 0 && C::V_BYTES % 1024 == 0, "image not a whole number of 1 KiB chunks");
+  constexpr int CPW = (NCH + 3) / 4;           // chunks per wave per tile
+  uint32_t doff[CPW];
 #pragma unroll
-  for (int i = 0; i < C::CPT; ++i) {
-    const int c = tid + 256 * i;
-    const int row = c / C::CPR, col = c % C::CPR;
-    koff[i] = (uint32_t)((row * p.k_st + col * 8) * 2);
-    voff[i] = (uint32_t)((row * p.v_st + col * 8) * 2);
-    ldsk[i] = row * C::KSTR + col * 16;
-    ldsv[i] = C::K_BYTES + row * C::VSTR + col * 16;
+  for (int i = 0; i < CPW; ++i) {
+    const int c = wave + 4 * i;
+    uint32_t off = 0xFFFFFFF0u;
+    if (c < KCH) {
+      const int x = c * 1024 + 16 * lane, row = x / C::KSTR, colb = x % C::KSTR;
+      if (colb < D * 2) off = (uint32_t)(row * p.k_st * 2 + colb);
+    } else if (c < NCH) {
+      const int x = (c - KCH) * 1024 + 16 * lane, row = x / C::VSTR, colb = x % C::VSTR;
+      if (colb < D * 2) off = (uint32_t)(row * p.v_st * 2 + colb);
+    }
+    doff[i] = off;
   }
-  u32x4 kst[C::CPT], vst[C::CPT];
   float bst = 0.f;
 
-  auto gload = [&](int t) {
+  auto gload = [&](int t) {                    // tile t -> LDS buffer t & 1 (asynchronous)
     const int key0 = t * C::BK;
     const int rows_left = S - key0;   // > 0 for every tile of the loop
     const auto ksrd = __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (int64_t)key0 * p.k_st), (short)0,
                                                         (int)((rows_left - 1) * p.k_st * 2 + D * 2), 0x00020000);
     const auto vsrd = __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (int64_t)key0 * p.v_st), (short)0,
                                                         (int)((rows_left - 1) * p.v_st * 2 + D * 2), 0x00020000);
+    char* base = smem + (t & 1) * C::STAGE;
 #pragma unroll
-    for (int i = 0; i < C::CPT; ++i) {
-      kst[i] = __builtin_amdgcn_raw_buffer_load_b128(ksrd, (int)koff[i], 0, 0);
-      vst[i] = __builtin_amdgcn_raw_buffer_load_b128(vsrd, (int)voff[i], 0, 0);
+    for (int i = 0; i < CPW; ++i) {
+      const int c = wave + 4 * i;
+      if (c < KCH)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (lds_void*)(base + c * 1024), 16, (int)doff[i], 0, 0, 0);
+      else if (c < NCH)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vsrd, (lds_void*)(base + c * 1024), 16, (int)doff[i], 0, 0, 0);
     }
     if (en_any && tid < C::BK) {
       const int wl = p.W - key0;
@@ -200,13 +215,8 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       bst = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(bsrd, tid * 4, 0, 0));   // scaled in swrite
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int buf) {                 // the bias row (register staged)
     char* base = smem + buf * C::STAGE;
-#pragma unroll
-    for (int i = 0; i < C::CPT; ++i) {
-      *reinterpret_cast<u32x4*>(base + ldsk[i]) = kst[i];
-      *reinterpret_cast<u32x4*>(base + ldsv[i]) = vst[i];
-    }
     if (en_any && tid < C::BK) reinterpret_cast<float*>(base + C::K_BYTES + C::V_BYTES)[tid] = bst * kLog2e;
   };
 
