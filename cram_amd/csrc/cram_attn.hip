@@ -13,11 +13,12 @@
 //                            O^T += V^T.P^T with P taken straight from the S^T
 //                            accumulator registers and V^T read with
 //                            ds_read_b64_tr_b16 from a row-major LDS image.
-//                            K/V/bias tiles register-staged into double-buffered
-//                            LDS (issue early, write late, one barrier per tile).
-//   decode_kernel<D,G>       q_len == 1, HBM-bound: 16 lanes per key row (16 B each),
-//                            all G query heads of a kv head per workgroup, optional
-//                            split over keys + combine_kernel.
+//                            K/V tiles land in double-buffered LDS by LDS-DMA
+//                            (buffer_load ... lds, issued one tile ahead, one barrier
+//                            per tile); a workgroup = the query heads of one kv head.
+//   decode_kernel<D,G>       q_len == 1, HBM-bound: 16 lanes per key row (16 B each,
+//                            DPP row reductions), all G query heads of a kv head per
+//                            workgroup, optional split over keys + combine_kernel.
 //   answer_logits_kernel     fp32 dot of hidden rows with gathered lm_head rows.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
