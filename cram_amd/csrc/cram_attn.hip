@@ -67,6 +67,19 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// Diagnostic build only (tools/stamp_prefill.hip defines CRAM_STAMPS): lane 0 of every wave writes
+// s_memtime at the phase boundaries of each tile to g_stamps[wid][wave][t][k]; the product library
+// compiles none of it.
+#ifdef CRAM_STAMPS
+__device__ unsigned long long* g_stamps;
+__device__ int g_stamp_tiles;
+#define CRAM_STAMP(k)                                                                                \
+  if (lane == 0 && t < g_stamp_tiles)                                                                \
+    g_stamps[(((size_t)wid * 4 + wave) * g_stamp_tiles + t) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+#else
+#define CRAM_STAMP(k)
+#endif
+
 // --------------------------------------------------------------------------------------------
 // prefill
 // --------------------------------------------------------------------------------------------
@@ -244,6 +257,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   __syncthreads();
 
   for (int t = 0; t < nt; ++t) {
+    CRAM_STAMP(0)
     if (t + 1 < nt) gload(t + 1);
     const int key0 = t * C::BK;
     if (wave_live && key0 <= wave_qpos_max) {
@@ -304,6 +318,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
         }
       }
       mx = half_max(mx);
+      CRAM_STAMP(1)
       const float mnew = fmaxf(m, mx);
       const float muse = (mnew == kNegInf) ? 0.f : mnew;
       const float alpha = fast_exp2(m - muse);
@@ -333,6 +348,7 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
           }
       }
       rs = half_sum(rs);
+      CRAM_STAMP(2)
       l = l * alpha + rs;
       m = mnew;
       // the running max rarely moves after the first tiles: skip the O rescale when alpha == 1 on
@@ -368,8 +384,10 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
         }
       }
     }
+    CRAM_STAMP(3)
     if (t + 1 < nt) swrite((t + 1) & 1);
     __syncthreads();
+    CRAM_STAMP(4)
   }
 
   if (qrow < Tq) {
