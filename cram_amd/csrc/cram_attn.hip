@@ -67,15 +67,13 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Diagnostic build only (tools/stamp_prefill.hip defines CRAM_STAMPS): lane 0 of every wave writes
-// s_memtime at the phase boundaries of each tile to g_stamps[wid][wave][t][k]; the product library
-// compiles none of it.
+// Diagnostic build only (tools/stamp_prefill.hip defines CRAM_STAMPS): every wave takes s_memtime at the
+// phase boundaries of each tile into registers, accumulates the per-phase deltas and lane 0 writes the
+// sums once at the end (no stores inside the loop: CDNA4's vmcnt counts stores, so per-tile stamp stores
+// would be waited for by the loop's own vmcnt).  The product library compiles none of it.
 #ifdef CRAM_STAMPS
-__device__ unsigned long long* g_stamps;
-__device__ int g_stamp_tiles;
-#define CRAM_STAMP(k)                                                                                \
-  if (lane == 0 && t < g_stamp_tiles)                                                                \
-    g_stamps[(((size_t)wid * 4 + wave) * g_stamp_tiles + t) * 8 + (k)] = __builtin_amdgcn_s_memtime();
+__device__ unsigned long long* g_stamps;   // [nblocks][4 waves][8]: phase sums 0..5, computed tiles
+#define CRAM_STAMP(k) st_[k] = __builtin_amdgcn_s_memtime();
 #else
 #define CRAM_STAMP(k)
 #endif
@@ -256,6 +254,9 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
   __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
   __syncthreads();
 
+#ifdef CRAM_STAMPS
+  unsigned long long st_[6] = {}, acc_[7] = {};
+#endif
   for (int t = 0; t < nt; ++t) {
     CRAM_STAMP(0)
     if (t + 1 < nt) gload(t + 1);
@@ -385,11 +386,26 @@ __global__ __launch_bounds__(256, 2) void prefill_kernel(PrefillParams p) {
       }
     }
     CRAM_STAMP(3)
+#ifdef CRAM_STAMPS
+    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);   // separates the DMA wait from the barrier wait
+    CRAM_STAMP(5)
+#endif
     if (t + 1 < nt) swrite((t + 1) & 1);
     __syncthreads();
     CRAM_STAMP(4)
+#ifdef CRAM_STAMPS
+    if (st_[1]) {                                   // a tile this wave computed
+      acc_[0] += st_[1] - st_[0]; acc_[1] += st_[2] - st_[1]; acc_[2] += st_[3] - st_[2];
+      acc_[3] += st_[5] - st_[3]; acc_[4] += st_[4] - st_[5]; acc_[6] += 1;
+    }
+    st_[1] = 0;
+#endif
   }
 
+#ifdef CRAM_STAMPS
+  if (lane == 0)
+    for (int k = 0; k < 7; ++k) g_stamps[((size_t)wid * 4 + wave) * 8 + k] = acc_[k];
+#endif
   if (qrow < Tq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
     __bf16* ob = p.o + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh + qrow * p.o_st;
