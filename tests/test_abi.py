@@ -62,3 +62,17 @@ def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", tmp_path / "missing.so")
     with pytest.raises(_lib.CrAMLibraryError):
         _lib.load()
+
+
+def test_plain_c_host_builds_and_links():
+    """examples/abi_demo.c: the header compiles as C11 and links against libcram_attn.so + the HIP runtime."""
+    import shutil
+    import subprocess
+    from cram_amd import build
+    build.build()
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    ex = os.path.join(REPO, "examples")
+    subprocess.run(["make", "-C", ex, "-s", "clean"], check=True)
+    subprocess.run(["make", "-C", ex, "-s"], check=True)
+    assert os.access(os.path.join(ex, "abi_demo"), os.X_OK)

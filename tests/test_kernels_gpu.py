@@ -360,3 +360,15 @@ def test_decode_full_size_sampled(gpu_device):
                 s[:W] += bias[b].double()
             ref = torch.softmax(s, 0) @ vv
             _check(out[b, h][None], ref[None])
+
+
+def test_plain_c_host_runs(gpu_device):
+    """The C-ABI driven from plain C (examples/abi_demo.c): biased prefill vs a double CPU loop + error path."""
+    import os
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-C", os.path.join(repo, "examples"), "-s"], check=True)
+    r = subprocess.run([os.path.join(repo, "examples", "abi_demo")], capture_output=True, text=True, timeout=120)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "max|err|" in r.stdout
