@@ -76,6 +76,8 @@ def main():
     ap.add_argument("--cpu-units", type=int, default=2)
     ap.add_argument("--blas", default="hipblaslt", choices=["hipblas", "hipblaslt"])
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPU) or gloo (rehearsal)")
+    ap.add_argument("--model", default=None, choices=["llama3-8b", "qwen2-7b", "llama2-13b"],
+                    help="override the config's model: llama2-13b = the reference's default model (fp16, MHA)")
     args = ap.parse_args()
 
     import torch
@@ -97,21 +99,26 @@ def main():
         torch.distributed.barrier()
     configure_blas(args.blas)
 
-    model = "qwen2-7b" if args.config == 4 else "llama3-8b"
-    spec = ModelSpec.qwen2_7b() if model == "qwen2-7b" else ModelSpec.llama3_8b()
+    model = args.model or ("qwen2-7b" if args.config == 4 else "llama3-8b")
+    spec = {"qwen2-7b": ModelSpec.qwen2_7b, "llama3-8b": ModelSpec.llama3_8b, "llama2-13b": ModelSpec.llama2_13b}[model]()
+    # torch_dtype="auto" of the real checkpoints: bf16 for Llama-3 / Qwen2, fp16 for Llama-2
+    mdtype = torch.float16 if model == "llama2-13b" else torch.bfloat16
     t0 = time.time()
-    eng = CrAMEngine.random(spec, dev, seed=1234, rope_theta=1e6 if model == "qwen2-7b" else 500000.0)
+    eng = CrAMEngine.random(spec, dev, seed=1234, rope_theta={"qwen2-7b": 1e6, "llama3-8b": 500000.0,
+                                                               "llama2-13b": 10000.0}[model], dtype=mdtype)
     torch.cuda.synchronize()
-    log(f"[rank {rank}] random-init {model} in {time.time() - t0:.1f}s")
+    log(f"[rank {rank}] random-init {model} ({mdtype}) in {time.time() - t0:.1f}s")
 
     from transformers import AutoTokenizer
+    # no Llama-2 tokenizer offline: its prompts use the Llama-3 BPE with the reference's raw Llama-2 template
     tok = AutoTokenizer.from_pretrained(os.path.join(REPO, "data", "tok_qwen" if model == "qwen2-7b" else "tok_llama3"))
-    name = "Qwen2-7B-Instruct" if model == "qwen2-7b" else "Meta-Llama-3-8B-Instruct"
+    name = {"qwen2-7b": "Qwen2-7B-Instruct", "llama3-8b": "Meta-Llama-3-8B-Instruct",
+            "llama2-13b": "Llama-2-13b-chat-hf"}[model]
     dsname = "trivia" if args.config == 4 else "nq"
     data = load_dataset(dsname)
     L, H = spec.num_layers, spec.num_heads
     result = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-              "higher_is_better": True, "vs_baseline": None, "dtype": "bf16"}
+              "higher_is_better": True, "vs_baseline": None, "dtype": "fp16" if mdtype == torch.float16 else "bf16"}
 
     # ------------------------------------------------------------------ IE sweep (config 3)
     ie = None
@@ -171,11 +178,12 @@ def main():
     # ------------------------------------------------------------------ batched reweighted decode (configs 2, 4, 5)
     decode = None
     if not args.no_decode:
-        if args.config == 4:
+        if model == "qwen2-7b":
             heads, heads_desc = {}, "all heads (no Qwen2 head fixture)"
         else:
-            heads = json.load(open(os.path.join(REPO, "data", "selected_heads.json")))["nq__llama3"]["heads"]
-            heads_desc = "nq/llama3 selected_heads top-894"
+            key = "nq__llama2_13b_chat" if model == "llama2-13b" else "nq__llama3"
+            heads = json.load(open(os.path.join(REPO, "data", "selected_heads.json")))[key]["heads"]
+            heads_desc = f"{key} selected_heads top-{sum(len(v) for v in heads.values())}"
         B = args.decode_batch if args.config != 5 else min(args.decode_batch, 16)
         qs, ps, ss = [], [], []
         for j in range(B):
@@ -193,6 +201,14 @@ def main():
         th = time.perf_counter()
         encs = spans.encode_batch(tok, name, qs, ps, ss)                     # host: prompts -> ids + fp16 weights
         host_ms = (time.perf_counter() - th) * 1e3
+        # the static KV cache is [L][B][Hkv][S_max][d] for K and V: MHA models (Llama-2-13b: 40 kv heads, 0.9 GB
+        # per 1.1k-token row) cap the batch at what fits next to the weights and the packed-prefill activations
+        s_max = max(ids.numel() for ids, _, _ in encs) + args.decode_tokens
+        per_row = 2 * spec.num_layers * spec.num_kv_heads * s_max * spec.head_dim * 2
+        cap = max(1, int(0.55 * torch.cuda.get_device_properties(dev).total_memory // per_row))
+        if cap < B:
+            log(f"[rank {rank}] decode batch {B} -> {cap} (KV cache {per_row / 2**20:.0f} MiB per row)")
+            B, encs = cap, encs[:cap]
         prompts = [ids.to(dev) for ids, _, _ in encs]
         ws = [w for _, w, _ in encs]
         eng.generate(prompts[:2], ws[:2], heads, max_new_tokens=4)          # warm the graph path
@@ -230,7 +246,7 @@ def main():
         cpu = {"value": r["units_per_s"], "unit": "heads/s", "cores": r["cores"], "kind": "port",
                "sample": f"{r['units']} IE units (hooked full forward + full-vocab logits + .item(), "
                          f"re_weighting.py:162-171) of NQ question {qi} at T'={ids.numel()}, after 1 un-hooked "
-                         f"forward; {r['seconds']:.1f}s; bf16 torch CPU; extrapolates linearly per unit"}
+                         f"forward; {r['seconds']:.1f}s; {result['dtype']} torch CPU; extrapolates linearly per unit"}
         del cpu_model
         log(f"[rank 0] cpu baseline {cpu['value']:.4f} heads/s on {cpu['cores']} cores ({time.time() - t0:.0f}s)")
 
@@ -242,7 +258,8 @@ def main():
                 ach = kt["flops"] / (kt["total_ms"] * 1e-3) / 1e12
                 roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                        "kernel": "prefill_kernel<128> (credibility-biased causal GQA flash attention, bf16 MFMA)",
+                        "kernel": f"prefill_kernel<{result['dtype']}, 128> (credibility-biased causal GQA flash "
+                                  f"attention, {result['dtype']} MFMA)",
                         "launches": kt["launches"], "avg_launch_ms": round(kt["avg_ms"], 4),
                         "flops_per_launch": kt["flops"] / kt["launches"],
                         "algorithmic_bytes_per_launch": kt["bytes"] / kt["launches"],
@@ -258,7 +275,7 @@ def main():
             dom = None
             if kg is not None and kg["total_ms"] > 0:
                 gtf = kg["flops"] / (kg["total_ms"] * 1e-3) / 1e12
-                dom = {"kernel": "hipBLASLt bf16 GEMMs (q/k/v, o, gate/up, down projections; F.linear)",
+                dom = {"kernel": f"hipBLASLt {result['dtype']} GEMMs (q/k/v, o, gate/up, down projections; F.linear)",
                        "bound": "mfma", "achieved": round(gtf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                        "frac": round(gtf / PEAK_BF16_TFLOPS, 4), "launches": kg["launches"],
                        "avg_launch_ms": round(kg["avg_ms"], 4), "flops_per_launch": kg["flops"] / kg["launches"],
@@ -269,8 +286,8 @@ def main():
             result.update({
                 "value": round(ie["value"], 3), "unit": "heads/s",
                 "ms_per_step": round(ie["elapsed"] * 1e3 / args.steps, 2), "scaling": "weak",
-                "data": "synthetic: random-init Llama-3-8B weights; rebuilt NQ-1000 prompts via offline BPE tokenizer",
-                "config": {"workload": "Llama-3-8B Find_Best_Heads IE sweep, 32 layers x 32 heads per question, "
+                "data": f"synthetic: random-init {name} weights; rebuilt NQ-1000 prompts via offline BPE tokenizer",
+                "config": {"workload": f"{name} Find_Best_Heads IE sweep, {L} layers x {H} heads per question, "
                                        "scores [0,1,1,1,1], 1 NQ question per GPU per step (config 3; decode = config 2)",
                            "model": model, "questions_per_step": world, "mean_prompt_tokens": round(ie["mean_T"], 1),
                            "parallelism": f"dp{world} question-sharded + RCCL all-gather of IE"},

@@ -17,6 +17,8 @@ _c_int32_p = POINTER(ctypes.c_int32)
 _c_uint8_p = POINTER(ctypes.c_uint8)
 _c_float_p = POINTER(c_float)
 
+ABI_VERSION = 2   # CRAM_ABI_VERSION of include/cram_attn.h
+
 # name -> (restype, argtypes); the exact export list of include/cram_attn.h
 SIGNATURES = {
     "cram_strerror": (ctypes.c_char_p, [c_int]),
@@ -28,12 +30,12 @@ SIGNATURES = {
         c_void_p, c_int64, c_int64, c_int64,
         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
         c_void_p, c_int64, c_void_p, c_int64, c_int,
-        c_void_p,
+        c_int, c_void_p,
     ]),
     "cram_attn_prefill_varlen": (c_int, [
         c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
         c_void_p, c_int64, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
-        c_void_p, c_int64, c_void_p, c_int64, c_int, c_void_p,
+        c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p,
     ]),
     "cram_attn_decode_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),
     "cram_attn_decode": (c_int, [
@@ -44,19 +46,19 @@ SIGNATURES = {
         c_int, c_int, c_int, c_int, c_void_p, c_int, c_float,
         c_void_p, c_int64, c_void_p, c_int64, c_int,
         c_int, c_void_p, c_size_t,
-        c_void_p,
+        c_int, c_void_p,
     ]),
     "cram_answer_logits": (c_int, [
-        c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+        c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
     ]),
     "cram_rmsnorm": (c_int, [
         c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int,
-        c_float, c_void_p,
+        c_float, c_int, c_void_p,
     ]),
     "cram_rope_inplace": (c_int, [
-        c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+        c_void_p, c_int64, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p,
     ]),
-    "cram_silu_mul": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p]),
+    "cram_silu_mul": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
     "cram_passage_weights": (c_int, [c_int] + [c_void_p] * 9),
 }
 
@@ -81,6 +83,9 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.cram_abi_version() != ABI_VERSION:
+        raise CrAMLibraryError(f"{LIB_PATH} exports ABI {lib.cram_abi_version()}, this binding needs {ABI_VERSION}: "
+                               "rebuild it with `python -m cram_amd.build`")
     _LIB = lib
     return lib
 

@@ -45,9 +45,9 @@ def cram_attention_forward(module: torch.nn.Module, query: torch.Tensor, key: to
     W = 0
     if cb is not None:
         bias, enable, W = cb.bias, cb.enable[module.layer_idx], cb.W
-    q = query if query.dtype == torch.bfloat16 else query.to(torch.bfloat16)
-    k = key if key.dtype == torch.bfloat16 else key.to(torch.bfloat16)
-    v = value if value.dtype == torch.bfloat16 else value.to(torch.bfloat16)
+    # bf16 / fp16 models run in their own dtype; fp32 ones (GPT-2 checkpoints) on bf16 operands
+    dt = query.dtype if query.dtype in ops.DTYPES else torch.bfloat16
+    q, k, v = (t if t.dtype == dt else t.to(dt) for t in (query, key, value))
     B, Hq, Tq, d = q.shape
     if Tq == 1:
         S = k.shape[2]

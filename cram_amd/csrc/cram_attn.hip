@@ -30,6 +30,8 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -43,6 +45,18 @@ constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegInf = -__builtin_huge_valf();
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// element type of q/k/v/o and of the MFMA operands: bf16 (Llama-3, Qwen2) or fp16 (Llama-2 checkpoints,
+// loaded with dtype="auto" as the reference does, re_weighting.py:22)
+template <typename T> struct Vec;
+template <> struct Vec<__bf16> { typedef bf16x8 x8; typedef bf16x4 x4; };
+template <> struct Vec<_Float16> { typedef f16x8 x8; typedef f16x4 x4; };
+__device__ __forceinline__ f32x16 mfma32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32x16(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 // value from lane l^32 combined with own value (lane halves exchanged by one permlane32 swap)
 __device__ __forceinline__ float half_max(float x) {
@@ -83,10 +97,10 @@ __device__ unsigned long long* g_stamps;   // [nblocks][4 waves][8]: phase sums 
 // prefill
 // --------------------------------------------------------------------------------------------
 struct PrefillParams {
-  const __bf16* q; int64_t q_sb, q_sh, q_st;
-  const __bf16* k; int64_t k_sb, k_sh, k_st;
-  const __bf16* v; int64_t v_sb, v_sh, v_st;
-  __bf16* o; int64_t o_sb, o_sh, o_st;
+  const void* q; int64_t q_sb, q_sh, q_st;
+  const void* k; int64_t k_sb, k_sh, k_st;
+  const void* v; int64_t v_sb, v_sh, v_st;
+  void* o; int64_t o_sb, o_sh, o_st;
   const float* bias; int64_t bias_sb;
   const uint8_t* enable; int64_t en_sb;
   int B, Hq, Hkv, Tq, S, W, q_pos0;
@@ -113,9 +127,11 @@ struct PrefillCfg {
   static constexpr int LDS = 2 * STAGE;
 };
 
-template <int D, int BK = 64, int OCC = 2>
+template <typename T, int D, int BK = 64, int OCC = 2>
 __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   using C = PrefillCfg<D, BK>;
+  using V8 = typename Vec<T>::x8;
+  using V4 = typename Vec<T>::x4;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
 
   // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each XCD a
@@ -152,9 +168,9 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   const int qrow = q_row0 + r;
   const int qpos = q_pos0 + qrow;
 
-  const __bf16* qb = p.q + b * p.q_sb + tok0 * p.q_st + hq * p.q_sh;
-  const __bf16* kbase = p.k + b * p.k_sb + tok0 * p.k_st + hkv * p.k_sh;
-  const __bf16* vbase = p.v + b * p.v_sb + tok0 * p.v_st + hkv * p.v_sh;
+  const T* qb = static_cast<const T*>(p.q) + b * p.q_sb + tok0 * p.q_st + hq * p.q_sh;
+  const T* kbase = static_cast<const T*>(p.k) + b * p.k_sb + tok0 * p.k_st + hkv * p.k_sh;
+  const T* vbase = static_cast<const T*>(p.v) + b * p.v_sb + tok0 * p.v_st + hkv * p.v_sh;
   // per-wave head enable; the workgroup stages the bias tile if any of its heads is enabled
   const bool has_bias = (p.bias != nullptr) && (p.enable != nullptr);
   const bool en = has_bias && p.enable[b * p.en_sb + hq] != 0;
@@ -164,14 +180,14 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   const float* brow = en_any ? p.bias + b * p.bias_sb : nullptr;
 
   // Q as the B operand of S^T = K.Q^T: lane (r, hh) holds Q[qrow][16ks + 8hh .. +7]
-  bf16x8 qf[D / 16];
+  V8 qf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
     if (qrow < Tq) {
-      qf[ks] = *reinterpret_cast<const bf16x8*>(qb + qrow * p.q_st + 16 * ks + 8 * hh);
+      qf[ks] = *reinterpret_cast<const V8*>(qb + qrow * p.q_st + 16 * ks + 8 * hh);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = (__bf16)0.f;
+      for (int j = 0; j < 8; ++j) qf[ks][j] = (T)0.f;
     }
   }
 
@@ -272,8 +288,8 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
       for (int kb = 0; kb < C::NKB; ++kb) {
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
-          sacc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[ks], ks == 0 ? zero16 : sacc[kb], 0, 0, 0);
+          const V8 a = *reinterpret_cast<const V8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
+          sacc[kb] = mfma32x16(a, qf[ks], ks == 0 ? zero16 : sacc[kb]);
         }
       }
       // scores (log2 units): scale, credibility bias, causal / length mask.  Wave-uniform split: a tile
@@ -370,9 +386,9 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
       for (int kb = 0; kb < C::NKB; ++kb) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 pb;
+          V8 pb;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) pb[j] = (__bf16)sacc[kb][8 * s + j];
+          for (int j = 0; j < 8; ++j) pb[j] = (T)sacc[kb][8 * s + j];
           const int key_a = kb * 32 + 16 * s + tr_key;
 #pragma unroll
           for (int db = 0; db < D / 32; ++db) {
@@ -382,8 +398,8 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
             const i16x4 r2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                 (lds_i16x4*)(vimg + (key_a + 8) * C::VSTR + col * 2));
             // whole-vector bit cast (per-element extraction of the tr result miscompiles on ROCm 7.2)
-            const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
-            oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, pb, oacc[db], 0, 0, 0);
+            const V8 af = __builtin_bit_cast(V8, __builtin_shufflevector(r1, r2, 0, 1, 2, 3, 4, 5, 6, 7));
+            oacc[db] = mfma32x16(af, pb, oacc[db]);
           }
         }
       }
@@ -411,15 +427,15 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
 #endif
   if (qrow < Tq) {
     const float inv = l > 0.f ? 1.f / l : 0.f;
-    __bf16* ob = p.o + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh + qrow * p.o_st;
+    T* ob = static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh + qrow * p.o_st;
 #pragma unroll
     for (int db = 0; db < D / 32; ++db)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        bf16x4 o4;
+        V4 o4;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o4[e] = (__bf16)(oacc[db][4 * g + e] * inv);
-        *reinterpret_cast<bf16x4*>(ob + db * 32 + 8 * g + 4 * hh) = o4;
+        for (int e = 0; e < 4; ++e) o4[e] = (T)(oacc[db][4 * g + e] * inv);
+        *reinterpret_cast<V4*>(ob + db * 32 + 8 * g + 4 * hh) = o4;
       }
   }
 }
@@ -428,10 +444,10 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
 // decode (q_len == 1)
 // --------------------------------------------------------------------------------------------
 struct DecodeParams {
-  const __bf16* q; int64_t q_sb, q_sh;
-  const __bf16* k; int64_t k_sb, k_sh, k_st;
-  const __bf16* v; int64_t v_sb, v_sh, v_st;
-  __bf16* o; int64_t o_sb, o_sh;
+  const void* q; int64_t q_sb, q_sh;
+  const void* k; int64_t k_sb, k_sh, k_st;
+  const void* v; int64_t v_sb, v_sh, v_st;
+  void* o; int64_t o_sb, o_sh;
   const float* bias; int64_t bias_sb;
   const uint8_t* enable; int64_t en_sb;
   const int32_t* seq_lens;
@@ -441,9 +457,10 @@ struct DecodeParams {
   float* ws_ml;  // [B][Hq][nsplit][2]  partial (max, sum)
 };
 
-template <int D, int G>
+template <typename T, int D, int G>
 __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
-  constexpr int LPK = D / 8;        // lanes per key row (8 bf16 = 16 B per lane)
+  using V8 = typename Vec<T>::x8;
+  constexpr int LPK = D / 8;        // lanes per key row (8 elements = 16 B per lane)
   constexpr int KPW = 64 / LPK;     // keys per wave-instruction
   constexpr int U = 4;              // keys per lane group per iteration
   constexpr int STEP = 4 * KPW;     // keys per workgroup per unrolled slot
@@ -465,14 +482,14 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const int hq = hkv * G + g;
-    const bf16x8 qq = *reinterpret_cast<const bf16x8*>(p.q + b * p.q_sb + hq * p.q_sh + li * 8);
+    const V8 qq = *reinterpret_cast<const V8*>(static_cast<const T*>(p.q) + b * p.q_sb + hq * p.q_sh + li * 8);
 #pragma unroll
     for (int j = 0; j < 8; ++j) qv[g][j] = (float)qq[j] * p.scale_log2;
     en[g] = (p.bias != nullptr) && (p.enable != nullptr) && p.enable[b * p.en_sb + hq] != 0;
   }
   const float* brow = p.bias ? p.bias + b * p.bias_sb : nullptr;
-  const __bf16* kbase = p.k + b * p.k_sb + hkv * p.k_sh + li * 8;
-  const __bf16* vbase = p.v + b * p.v_sb + hkv * p.v_sh + li * 8;
+  const T* kbase = static_cast<const T*>(p.k) + b * p.k_sb + hkv * p.k_sh + li * 8;
+  const T* vbase = static_cast<const T*>(p.v) + b * p.v_sb + hkv * p.v_sh + li * 8;
 
   float m[G], l[G], acc[G][8];
 #pragma unroll
@@ -485,17 +502,17 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
 
   // K/V rows of the next iteration are loaded while the current one is computed (register double
   // buffer): every wave keeps 2 x U x 2 16-byte loads in flight instead of stalling on each batch
-  bf16x8 kn[U], vn[U];
+  V8 kn[U], vn[U];
   auto load_keys = [&](int kb0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int key = kb0 + u * STEP;
       if (key < k_end) {
-        kn[u] = *reinterpret_cast<const bf16x8*>(kbase + key * p.k_st);
-        vn[u] = *reinterpret_cast<const bf16x8*>(vbase + key * p.v_st);
+        kn[u] = *reinterpret_cast<const V8*>(kbase + key * p.k_st);
+        vn[u] = *reinterpret_cast<const V8*>(vbase + key * p.v_st);
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { kn[u][j] = (__bf16)0.f; vn[u][j] = (__bf16)0.f; }
+        for (int j = 0; j < 8; ++j) { kn[u][j] = (T)0.f; vn[u][j] = (T)0.f; }
       }
     }
   };
@@ -503,7 +520,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
   if (PF) load_keys(k_begin + wave * KPW + grp);
   for (int key_base = k_begin + wave * KPW + grp; key_base < k_end; key_base += U * STEP) {
     if (!PF) load_keys(key_base);
-    bf16x8 kr[U], vr[U];
+    V8 kr[U], vr[U];
     bool valid[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -593,7 +610,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
     }
     const int hq = hkv * G + g;
     if (nsplit == 1) {
-      p.o[b * p.o_sb + hq * p.o_sh + dd] = (__bf16)(L > 0.f ? O / L : 0.f);
+      static_cast<T*>(p.o)[b * p.o_sb + hq * p.o_sh + dd] = (T)(L > 0.f ? O / L : 0.f);
     } else {
       const int64_t slot = ((int64_t)(b * p.Hq + hq) * nsplit + split);
       p.ws_o[slot * D + dd] = O;
@@ -602,7 +619,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
   }
 }
 
-template <int D>
+template <typename T, int D>
 __global__ __launch_bounds__(D) void decode_combine_kernel(DecodeParams p, int nsplit) {
   const int hq = blockIdx.x, b = blockIdx.y, dd = threadIdx.x;
   const int64_t slot0 = (int64_t)(b * p.Hq + hq) * nsplit;
@@ -615,30 +632,32 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(DecodeParams p, int n
     L += p.ws_ml[(slot0 + s) * 2 + 1] * a;
     O += p.ws_o[(slot0 + s) * D + dd] * a;
   }
-  p.o[b * p.o_sb + hq * p.o_sh + dd] = (__bf16)(L > 0.f ? O / L : 0.f);
+  static_cast<T*>(p.o)[b * p.o_sb + hq * p.o_sh + dd] = (T)(L > 0.f ? O / L : 0.f);
 }
 
 // --------------------------------------------------------------------------------------------
 // answer-token logits
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void answer_logits_kernel(const __bf16* h, int64_t h_rs, const __bf16* w,
-                                                            int64_t w_rs, const int32_t* ids, int n, int D,
-                                                            int round_bf16, float* out) {
+template <typename T>
+__global__ __launch_bounds__(256) void answer_logits_kernel(const T* h, int64_t h_rs, const T* w, int64_t w_rs,
+                                                            const int32_t* ids, int n, int D, int round_logits,
+                                                            float* out) {
+  using V8 = typename Vec<T>::x8;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (row >= n) return;
-  const __bf16* hr = h + row * h_rs;
-  const __bf16* wr = w + (int64_t)ids[row] * w_rs;
+  const T* hr = h + row * h_rs;
+  const T* wr = w + (int64_t)ids[row] * w_rs;
   float acc = 0.f;
   for (int d0 = lane * 8; d0 < D; d0 += 512) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(hr + d0);
-    const bf16x8 c = *reinterpret_cast<const bf16x8*>(wr + d0);
+    const V8 a = *reinterpret_cast<const V8*>(hr + d0);
+    const V8 c = *reinterpret_cast<const V8*>(wr + d0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc += (float)a[j] * (float)c[j];
   }
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if (lane == 0) out[row] = round_bf16 ? (float)(__bf16)acc : acc;
+  if (lane == 0) out[row] = round_logits ? (float)(T)acc : acc;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -647,7 +666,7 @@ __global__ __launch_bounds__(256) void answer_logits_kernel(const __bf16* h, int
 inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
 inline bool m8(int64_t s) { return (s & 7) == 0; }
 
-template <int D>
+template <typename T, int D>
 int launch_prefill(PrefillParams& p, hipStream_t stream) {
   const int G = p.Hq / p.Hkv;
   p.hp = (G % 4 == 0) ? 4 : (G % 2 == 0) ? 2 : 1;
@@ -661,34 +680,42 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // (tools/ie_noise_probe.py), so 64-key tiles at two waves per SIMD stay the default
   const char* e = getenv("CRAM_PREFILL_VARIANT");
   if (D == 128 && e && e[0] == '3')
-    hipLaunchKernelGGL((prefill_kernel<D, 32, 3>), dim3(p.nblocks), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((prefill_kernel<T, D, 32, 3>), dim3(p.nblocks), dim3(256), 0, stream, p);
   else
-    hipLaunchKernelGGL((prefill_kernel<D, 64, 2>), dim3(p.nblocks), dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((prefill_kernel<T, D, 64, 2>), dim3(p.nblocks), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 
-template <int D, int G>
+int dispatch_prefill(PrefillParams& p, int d, int dtype, hipStream_t stream) {
+  if (dtype == CRAM_DTYPE_BF16)
+    return d == 128 ? launch_prefill<__bf16, 128>(p, stream) : launch_prefill<__bf16, 64>(p, stream);
+  return d == 128 ? launch_prefill<_Float16, 128>(p, stream) : launch_prefill<_Float16, 64>(p, stream);
+}
+
+template <typename T, int D, int G>
 int launch_decode_g(DecodeParams& p, int nsplit, hipStream_t stream) {
-  hipLaunchKernelGGL((decode_kernel<D, G>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((decode_kernel<T, D, G>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
   if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
   if (nsplit > 1) {
-    hipLaunchKernelGGL(decode_combine_kernel<D>, dim3(p.Hq, p.B), dim3(D), 0, stream, p, nsplit);
+    hipLaunchKernelGGL((decode_combine_kernel<T, D>), dim3(p.Hq, p.B), dim3(D), 0, stream, p, nsplit);
     if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
   }
   return CRAM_OK;
 }
 
-template <int D>
+template <typename T, int D>
 int launch_decode(DecodeParams& p, int G, int nsplit, hipStream_t stream) {
   switch (G) {
-    case 1: return launch_decode_g<D, 1>(p, nsplit, stream);
-    case 2: return launch_decode_g<D, 2>(p, nsplit, stream);
-    case 4: return launch_decode_g<D, 4>(p, nsplit, stream);
-    case 7: return launch_decode_g<D, 7>(p, nsplit, stream);
-    case 8: return launch_decode_g<D, 8>(p, nsplit, stream);
+    case 1: return launch_decode_g<T, D, 1>(p, nsplit, stream);
+    case 2: return launch_decode_g<T, D, 2>(p, nsplit, stream);
+    case 4: return launch_decode_g<T, D, 4>(p, nsplit, stream);
+    case 7: return launch_decode_g<T, D, 7>(p, nsplit, stream);
+    case 8: return launch_decode_g<T, D, 8>(p, nsplit, stream);
     default: return CRAM_ERR_UNSUPPORTED;
   }
 }
+
+inline bool dtype_ok(int dtype) { return dtype == CRAM_DTYPE_BF16 || dtype == CRAM_DTYPE_F16; }
 
 }  // namespace
 
@@ -698,7 +725,7 @@ const char* cram_strerror(int code) {
   switch (code) {
     case CRAM_OK: return "ok";
     case CRAM_ERR_INVALID_ARG: return "invalid argument";
-    case CRAM_ERR_UNSUPPORTED: return "unsupported head dim or GQA group size";
+    case CRAM_ERR_UNSUPPORTED: return "unsupported head dim, GQA group size or element type";
     case CRAM_ERR_ALIGNMENT: return "stride not a multiple of 8 elements or pointer not 16-byte aligned";
     case CRAM_ERR_LAUNCH: return "kernel launch failed";
     case CRAM_ERR_WORKSPACE: return "split-S workspace missing or too small";
@@ -706,16 +733,16 @@ const char* cram_strerror(int code) {
   }
 }
 
-int cram_abi_version(void) { return 1; }
+int cram_abi_version(void) { return CRAM_ABI_VERSION; }
 
 int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sb,
                       int64_t k_sh, int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st, void* o,
                       int64_t o_sb, int64_t o_sh, int64_t o_st, int B, int Hq, int Hkv, int Tq, int S, int d,
                       int q_pos0, float scale, const float* bias, int64_t bias_sb, const uint8_t* enable,
-                      int64_t en_sb, int W, cram_stream_t stream) {
+                      int64_t en_sb, int W, int dtype, cram_stream_t stream) {
   if (!q || !k || !v || !o) return CRAM_ERR_INVALID_ARG;
   if (B <= 0 || Hq <= 0 || Hkv <= 0 || Tq <= 0 || S <= 0 || Hq % Hkv != 0 || q_pos0 < 0) return CRAM_ERR_INVALID_ARG;
-  if (d != 64 && d != 128) return CRAM_ERR_UNSUPPORTED;
+  if ((d != 64 && d != 128) || !dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return CRAM_ERR_ALIGNMENT;
   if (!m8(q_sb) || !m8(q_sh) || !m8(q_st) || !m8(k_sb) || !m8(k_sh) || !m8(k_st) || !m8(v_sb) || !m8(v_sh) ||
       !m8(v_st) || !m8(o_sb) || !m8(o_sh) || !m8(o_st))
@@ -725,26 +752,26 @@ int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, c
   if ((int64_t)S * (k_st > v_st ? k_st : v_st) * 2 + 2 * d >= (1ll << 31) || (int64_t)W * 4 >= (1ll << 31))
     return CRAM_ERR_UNSUPPORTED;
   PrefillParams p;
-  p.q = (const __bf16*)q; p.q_sb = q_sb; p.q_sh = q_sh; p.q_st = q_st;
-  p.k = (const __bf16*)k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
-  p.v = (const __bf16*)v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
-  p.o = (__bf16*)o; p.o_sb = o_sb; p.o_sh = o_sh; p.o_st = o_st;
+  p.q = q; p.q_sb = q_sb; p.q_sh = q_sh; p.q_st = q_st;
+  p.k = k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = o; p.o_sb = o_sb; p.o_sh = o_sh; p.o_st = o_st;
   p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
   p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = Tq; p.S = S; p.W = bias ? W : 0; p.q_pos0 = q_pos0;
   p.scale_log2 = scale * kLog2e;
   p.cu = nullptr;
-  return d == 128 ? launch_prefill<128>(p, (hipStream_t)stream) : launch_prefill<64>(p, (hipStream_t)stream);
+  return dispatch_prefill(p, d, dtype, (hipStream_t)stream);
 }
 
 int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sh, int64_t k_st,
                              const void* v, int64_t v_sh, int64_t v_st, void* o, int64_t o_sh, int64_t o_st,
                              const int32_t* cu_seqlens, int B, int max_len, int Hq, int Hkv, int d, float scale,
                              const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
-                             cram_stream_t stream) {
+                             int dtype, cram_stream_t stream) {
   if (!q || !k || !v || !o || !cu_seqlens) return CRAM_ERR_INVALID_ARG;
   if (B <= 0 || Hq <= 0 || Hkv <= 0 || max_len <= 0 || Hq % Hkv != 0) return CRAM_ERR_INVALID_ARG;
-  if (d != 64 && d != 128) return CRAM_ERR_UNSUPPORTED;
+  if ((d != 64 && d != 128) || !dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return CRAM_ERR_ALIGNMENT;
   if (!m8(q_sh) || !m8(q_st) || !m8(k_sh) || !m8(k_st) || !m8(v_sh) || !m8(v_st) || !m8(o_sh) || !m8(o_st))
     return CRAM_ERR_ALIGNMENT;
@@ -752,16 +779,16 @@ int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const vo
   if ((int64_t)max_len * (k_st > v_st ? k_st : v_st) * 2 + 2 * d >= (1ll << 31) || (int64_t)W * 4 >= (1ll << 31))
     return CRAM_ERR_UNSUPPORTED;
   PrefillParams p;
-  p.q = (const __bf16*)q; p.q_sb = 0; p.q_sh = q_sh; p.q_st = q_st;
-  p.k = (const __bf16*)k; p.k_sb = 0; p.k_sh = k_sh; p.k_st = k_st;
-  p.v = (const __bf16*)v; p.v_sb = 0; p.v_sh = v_sh; p.v_st = v_st;
-  p.o = (__bf16*)o; p.o_sb = 0; p.o_sh = o_sh; p.o_st = o_st;
+  p.q = q; p.q_sb = 0; p.q_sh = q_sh; p.q_st = q_st;
+  p.k = k; p.k_sb = 0; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = v; p.v_sb = 0; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = o; p.o_sb = 0; p.o_sh = o_sh; p.o_st = o_st;
   p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
   p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = max_len; p.S = max_len; p.W = bias ? W : 0; p.q_pos0 = 0;
   p.scale_log2 = scale * kLog2e;
   p.cu = cu_seqlens;
-  return d == 128 ? launch_prefill<128>(p, (hipStream_t)stream) : launch_prefill<64>(p, (hipStream_t)stream);
+  return dispatch_prefill(p, d, dtype, (hipStream_t)stream);
 }
 
 size_t cram_attn_decode_workspace_size(int B, int Hq, int d, int num_splits) {
@@ -773,21 +800,21 @@ int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh, const void* k, i
                      int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st, void* o, int64_t o_sb,
                      int64_t o_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d, float scale,
                      const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
-                     int num_splits, void* workspace, size_t workspace_bytes, cram_stream_t stream) {
+                     int num_splits, void* workspace, size_t workspace_bytes, int dtype, cram_stream_t stream) {
   if (!q || !k || !v || !o) return CRAM_ERR_INVALID_ARG;
   if (B <= 0 || Hq <= 0 || Hkv <= 0 || S <= 0 || Hq % Hkv != 0 || num_splits <= 0 || B > 65535 ||
       num_splits > 65535)
     return CRAM_ERR_INVALID_ARG;
-  if (d != 64 && d != 128) return CRAM_ERR_UNSUPPORTED;
+  if ((d != 64 && d != 128) || !dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (!al16(q) || !al16(k) || !al16(v)) return CRAM_ERR_ALIGNMENT;
   if (!m8(q_sb) || !m8(q_sh) || !m8(k_sb) || !m8(k_sh) || !m8(k_st) || !m8(v_sb) || !m8(v_sh) || !m8(v_st))
     return CRAM_ERR_ALIGNMENT;
   if (bias && W < 0) return CRAM_ERR_INVALID_ARG;
   DecodeParams p;
-  p.q = (const __bf16*)q; p.q_sb = q_sb; p.q_sh = q_sh;
-  p.k = (const __bf16*)k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
-  p.v = (const __bf16*)v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
-  p.o = (__bf16*)o; p.o_sb = o_sb; p.o_sh = o_sh;
+  p.q = q; p.q_sb = q_sb; p.q_sh = q_sh;
+  p.k = k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = o; p.o_sb = o_sb; p.o_sh = o_sh;
   p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
   p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
   p.seq_lens = seq_lens;
@@ -801,17 +828,27 @@ int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh, const void* k, i
     p.ws_ml = p.ws_o + (size_t)B * Hq * num_splits * d;
   }
   const int G = Hq / Hkv;
-  return d == 128 ? launch_decode<128>(p, G, num_splits, (hipStream_t)stream)
-                  : launch_decode<64>(p, G, num_splits, (hipStream_t)stream);
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRAM_DTYPE_BF16)
+    return d == 128 ? launch_decode<__bf16, 128>(p, G, num_splits, st) : launch_decode<__bf16, 64>(p, G, num_splits, st);
+  return d == 128 ? launch_decode<_Float16, 128>(p, G, num_splits, st)
+                  : launch_decode<_Float16, 64>(p, G, num_splits, st);
 }
 
 int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64_t w_rs, const int32_t* ids, int n,
-                       int D, int round_bf16, float* out, cram_stream_t stream) {
+                       int D, int round_logits, float* out, int dtype, cram_stream_t stream) {
   if (!hidden || !w_lm || !ids || !out || n < 0 || D <= 0) return CRAM_ERR_INVALID_ARG;
+  if (!dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (n == 0) return CRAM_OK;
   if ((D & 7) || !m8(h_rs) || !m8(w_rs) || !al16(hidden) || !al16(w_lm)) return CRAM_ERR_ALIGNMENT;
-  hipLaunchKernelGGL(answer_logits_kernel, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     (const __bf16*)hidden, h_rs, (const __bf16*)w_lm, w_rs, ids, n, D, round_bf16, out);
+  const dim3 g((n + 3) / 4);
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRAM_DTYPE_BF16)
+    hipLaunchKernelGGL(answer_logits_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)hidden, h_rs,
+                       (const __bf16*)w_lm, w_rs, ids, n, D, round_logits, out);
+  else
+    hipLaunchKernelGGL(answer_logits_kernel<_Float16>, g, dim3(256), 0, st, (const _Float16*)hidden, h_rs,
+                       (const _Float16*)w_lm, w_rs, ids, n, D, round_logits, out);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 

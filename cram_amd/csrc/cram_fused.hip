@@ -5,11 +5,12 @@
 // cast, pow, mean, rsqrt, mul, cast, mul; RoPE: mul, cat, neg, mul, add; MLP:
 // silu, mul).  These kernels do each group in one pass and keep transformers'
 // rounding points (LlamaRMSNorm, apply_rotary_pos_emb, LlamaMLP), so results
-// equal the reference's op sequence up to the fp32 order of the RMS reduction:
-//   rmsnorm      y = bf16(w * bf16(x * rsqrt(mean(x^2) + eps)))      [+ fused residual add]
-//   rope         x' = bf16(bf16(x * cos) + bf16(rotate_half(x) * sin))  in place on the QKV buffer
-//   silu_mul     y = bf16(bf16(silu(g)) * u)
-// All loads/stores are 16 B per lane (8 bf16).
+// equal the reference's op sequence up to the fp32 order of the RMS reduction (rnd = round to the
+// model dtype, bf16 or fp16):
+//   rmsnorm      y = rnd(w * rnd(x * rsqrt(mean(x^2) + eps)))      [+ fused residual add]
+//   rope         x' = rnd(rnd(x * cos) + rnd(rotate_half(x) * sin))  in place on the QKV buffer
+//   silu_mul     y = rnd(rnd(silu(g)) * u)
+// All loads/stores are 16 B per lane (8 elements).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -18,6 +19,10 @@
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <typename T> struct Vec;
+template <> struct Vec<__bf16> { typedef bf16x8 x8; };
+template <> struct Vec<_Float16> { typedef f16x8 x8; };
 
 // round-to-nearest-even to bf16 and back, by integer arithmetic: the compiler folds a
 // (float)(__bf16)x pair away in some contexts (measured on ROCm 7.2: 1-ulp RoPE mismatches),
@@ -27,6 +32,16 @@ __device__ __forceinline__ float bfr(float x) {
   u = (u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u;
   return __uint_as_float(u);
 }
+// fp16: the hardware conversion (RNE, subnormals kept), its result pinned in a register so the
+// round trip cannot be folded away either
+__device__ __forceinline__ float hfr(float x) {
+  unsigned short b = __builtin_bit_cast(unsigned short, (_Float16)x);
+  asm volatile("" : "+v"(b));
+  return (float)__builtin_bit_cast(_Float16, b);
+}
+template <typename T> __device__ __forceinline__ float rnd(float x);
+template <> __device__ __forceinline__ float rnd<__bf16>(float x) { return bfr(x); }
+template <> __device__ __forceinline__ float rnd<_Float16>(float x) { return hfr(x); }
 
 template <int NT>
 __device__ __forceinline__ float block_sum(float v, float* red) {
@@ -42,27 +57,28 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 
 // one workgroup per row; VPT 8-element vectors per thread
-template <int NT, int VPT>
-__global__ __launch_bounds__(NT) void rmsnorm_kernel(const __bf16* __restrict__ x, int64_t x_rs,
-                                                     const __bf16* __restrict__ res, int64_t r_rs,
-                                                     __bf16* __restrict__ h_out, int64_t h_rs,
-                                                     const __bf16* __restrict__ w, __bf16* __restrict__ y,
+template <typename T, int NT, int VPT>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(const T* __restrict__ x, int64_t x_rs,
+                                                     const T* __restrict__ res, int64_t r_rs,
+                                                     T* __restrict__ h_out, int64_t h_rs,
+                                                     const T* __restrict__ w, T* __restrict__ y,
                                                      int64_t y_rs, int D, float eps) {
+  using V8 = typename Vec<T>::x8;
   __shared__ float red[NT / 64];
   const int64_t row = blockIdx.x;
-  const __bf16* xr = x + row * x_rs;
-  bf16x8 v[VPT];
+  const T* xr = x + row * x_rs;
+  V8 v[VPT];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = (threadIdx.x + i * NT) * 8;
     if (c < D) {
-      v[i] = *reinterpret_cast<const bf16x8*>(xr + c);
+      v[i] = *reinterpret_cast<const V8*>(xr + c);
       if (res) {
-        const bf16x8 r = *reinterpret_cast<const bf16x8*>(res + row * r_rs + c);
+        const V8 r = *reinterpret_cast<const V8*>(res + row * r_rs + c);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[i][j] = (__bf16)((float)v[i][j] + (float)r[j]);
-        *reinterpret_cast<bf16x8*>(h_out + row * h_rs + c) = v[i];
+        for (int j = 0; j < 8; ++j) v[i][j] = (T)((float)v[i][j] + (float)r[j]);
+        *reinterpret_cast<V8*>(h_out + row * h_rs + c) = v[i];
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -77,20 +93,22 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(const __bf16* __restrict__ 
   for (int i = 0; i < VPT; ++i) {
     const int c = (threadIdx.x + i * NT) * 8;
     if (c < D) {
-      const bf16x8 ww = *reinterpret_cast<const bf16x8*>(w + c);
-      bf16x8 o;
+      const V8 ww = *reinterpret_cast<const V8*>(w + c);
+      V8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (__bf16)((float)ww[j] * bfr((float)v[i][j] * inv));
-      *reinterpret_cast<bf16x8*>(y + row * y_rs + c) = o;
+      for (int j = 0; j < 8; ++j) o[j] = (T)((float)ww[j] * rnd<T>((float)v[i][j] * inv));
+      *reinterpret_cast<V8*>(y + row * y_rs + c) = o;
     }
   }
 }
 
 // one thread = 8 rotation pairs (i, i + d/2) of one head of one row
-__global__ __launch_bounds__(256) void rope_kernel(__bf16* __restrict__ qkv, int64_t rs, int rows, int T, int heads,
-                                                   int d, const __bf16* __restrict__ cos_t,
-                                                   const __bf16* __restrict__ sin_t, int64_t tab_rs,
+template <typename E>
+__global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t rs, int rows, int T, int heads,
+                                                   int d, const E* __restrict__ cos_t,
+                                                   const E* __restrict__ sin_t, int64_t tab_rs,
                                                    const int64_t* __restrict__ pos) {
+  using V8 = typename Vec<E>::x8;
   const unsigned half = (unsigned)d >> 1, vpp = half >> 3;  // vectors per half-row
   const unsigned gid = blockIdx.x * 256u + threadIdx.x;      // host guarantees rows*heads*vpp < 2^31
   if (gid >= (unsigned)rows * (unsigned)heads * vpp) return;
@@ -100,51 +118,65 @@ __global__ __launch_bounds__(256) void rope_kernel(__bf16* __restrict__ qkv, int
   const unsigned row32 = rh / (unsigned)heads;
   const int64_t row = row32;
   const int64_t p = pos ? pos[row] : (int64_t)(row32 % (unsigned)T);
-  __bf16* base = qkv + row * rs + (int64_t)h * d + vi * 8;
-  const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(base);
-  const bf16x8 x2 = *reinterpret_cast<const bf16x8*>(base + half);
-  const __bf16* ct = cos_t + p * tab_rs + vi * 8;
-  const __bf16* st = sin_t + p * tab_rs + vi * 8;
-  const bf16x8 c1 = *reinterpret_cast<const bf16x8*>(ct), c2 = *reinterpret_cast<const bf16x8*>(ct + half);
-  const bf16x8 s1 = *reinterpret_cast<const bf16x8*>(st), s2 = *reinterpret_cast<const bf16x8*>(st + half);
-  bf16x8 o1, o2;
+  E* base = qkv + row * rs + (int64_t)h * d + vi * 8;
+  const V8 x1 = *reinterpret_cast<const V8*>(base);
+  const V8 x2 = *reinterpret_cast<const V8*>(base + half);
+  const E* ct = cos_t + p * tab_rs + vi * 8;
+  const E* st = sin_t + p * tab_rs + vi * 8;
+  const V8 c1 = *reinterpret_cast<const V8*>(ct), c2 = *reinterpret_cast<const V8*>(ct + half);
+  const V8 s1 = *reinterpret_cast<const V8*>(st), s2 = *reinterpret_cast<const V8*>(st + half);
+  V8 o1, o2;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float a = (float)x1[j], b = (float)x2[j];
     // first half: x1*cos - x2*sin ; second half: x2*cos + x1*sin   (rotate_half = cat(-x2, x1))
-    o1[j] = (__bf16)(bfr(a * (float)c1[j]) + bfr(-b * (float)s1[j]));
-    o2[j] = (__bf16)(bfr(b * (float)c2[j]) + bfr(a * (float)s2[j]));
+    o1[j] = (E)(rnd<E>(a * (float)c1[j]) + rnd<E>(-b * (float)s1[j]));
+    o2[j] = (E)(rnd<E>(b * (float)c2[j]) + rnd<E>(a * (float)s2[j]));
   }
-  *reinterpret_cast<bf16x8*>(base) = o1;
-  *reinterpret_cast<bf16x8*>(base + half) = o2;
+  *reinterpret_cast<V8*>(base) = o1;
+  *reinterpret_cast<V8*>(base + half) = o2;
 }
 
-__global__ __launch_bounds__(256) void silu_mul_kernel(const __bf16* __restrict__ gu, int64_t gu_rs,
-                                                       __bf16* __restrict__ y, int64_t y_rs, int rows, int F) {
+template <typename T>
+__global__ __launch_bounds__(256) void silu_mul_kernel(const T* __restrict__ gu, int64_t gu_rs,
+                                                       T* __restrict__ y, int64_t y_rs, int rows, int F) {
+  using V8 = typename Vec<T>::x8;
   const unsigned vpr = (unsigned)F >> 3;
   const unsigned gid = blockIdx.x * 256u + threadIdx.x;      // host guarantees rows*vpr < 2^31
   if (gid >= (unsigned)rows * vpr) return;
   const int64_t row = gid / vpr;
   const int c = (int)(gid % vpr) * 8;
-  const bf16x8 g = *reinterpret_cast<const bf16x8*>(gu + row * gu_rs + c);
-  const bf16x8 u = *reinterpret_cast<const bf16x8*>(gu + row * gu_rs + F + c);
-  bf16x8 o;
+  const V8 g = *reinterpret_cast<const V8*>(gu + row * gu_rs + c);
+  const V8 u = *reinterpret_cast<const V8*>(gu + row * gu_rs + F + c);
+  V8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float x = (float)g[j];
-    const float s = bfr(x / (1.0f + expf(-x)));
-    o[j] = (__bf16)(s * (float)u[j]);
+    const float s = rnd<T>(x / (1.0f + expf(-x)));
+    o[j] = (T)(s * (float)u[j]);
   }
-  *reinterpret_cast<bf16x8*>(y + row * y_rs + c) = o;
+  *reinterpret_cast<V8*>(y + row * y_rs + c) = o;
 }
 
 inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 inline bool m8(int64_t s) { return (s & 7) == 0; }
 
-template <int NT, int VPT>
-void launch_rms(dim3 g, hipStream_t st, const __bf16* x, int64_t x_rs, const __bf16* r, int64_t r_rs, __bf16* h,
-                int64_t h_rs, const __bf16* w, __bf16* y, int64_t y_rs, int D, float eps) {
-  hipLaunchKernelGGL((rmsnorm_kernel<NT, VPT>), g, dim3(NT), 0, st, x, x_rs, r, r_rs, h, h_rs, w, y, y_rs, D, eps);
+inline bool dtype_ok(int dtype) { return dtype == CRAM_DTYPE_BF16 || dtype == CRAM_DTYPE_F16; }
+
+template <typename T>
+int launch_rms(int rows, hipStream_t st, const void* x, int64_t x_rs, const void* r, int64_t r_rs, void* h,
+               int64_t h_rs, const void* w, void* y, int64_t y_rs, int D, float eps) {
+  const int vec = D / 8;
+  const dim3 g(rows);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, g, dim3(256), 0, st, (const T*)x, x_rs, (const T*)r, r_rs, (T*)h, h_rs, (const T*)w,
+                       (T*)y, y_rs, D, eps);
+  };
+  if (vec <= 256) go(rmsnorm_kernel<T, 256, 1>);
+  else if (vec <= 512) go(rmsnorm_kernel<T, 256, 2>);
+  else if (vec <= 1024) go(rmsnorm_kernel<T, 256, 4>);
+  else return CRAM_ERR_UNSUPPORTED;
+  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 
 }  // namespace
@@ -152,46 +184,54 @@ void launch_rms(dim3 g, hipStream_t st, const __bf16* x, int64_t x_rs, const __b
 extern "C" {
 
 int cram_rmsnorm(const void* x, int64_t x_rs, const void* residual, int64_t r_rs, void* h_out, int64_t h_rs,
-                 const void* w, void* y, int64_t y_rs, int rows, int D, float eps, cram_stream_t stream) {
+                 const void* w, void* y, int64_t y_rs, int rows, int D, float eps, int dtype, cram_stream_t stream) {
   if (!x || !w || !y || rows < 0 || D <= 0 || (residual && !h_out)) return CRAM_ERR_INVALID_ARG;
+  if (!dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (rows == 0) return CRAM_OK;
   if ((D & 7) || !m8(x_rs) || !m8(y_rs) || !al16(x) || !al16(y) || !al16(w)) return CRAM_ERR_ALIGNMENT;
   if (residual && (!m8(r_rs) || !m8(h_rs) || !al16(residual) || !al16(h_out))) return CRAM_ERR_ALIGNMENT;
-  const int vec = D / 8;
   const hipStream_t st = (hipStream_t)stream;
-  const dim3 g(rows);
-  if (vec <= 256) launch_rms<256, 1>(g, st, (const __bf16*)x, x_rs, (const __bf16*)residual, r_rs, (__bf16*)h_out,
-                                     h_rs, (const __bf16*)w, (__bf16*)y, y_rs, D, eps);
-  else if (vec <= 512) launch_rms<256, 2>(g, st, (const __bf16*)x, x_rs, (const __bf16*)residual, r_rs,
-                                          (__bf16*)h_out, h_rs, (const __bf16*)w, (__bf16*)y, y_rs, D, eps);
-  else if (vec <= 1024) launch_rms<256, 4>(g, st, (const __bf16*)x, x_rs, (const __bf16*)residual, r_rs,
-                                           (__bf16*)h_out, h_rs, (const __bf16*)w, (__bf16*)y, y_rs, D, eps);
-  else return CRAM_ERR_UNSUPPORTED;
-  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+  return dtype == CRAM_DTYPE_BF16
+             ? launch_rms<__bf16>(rows, st, x, x_rs, residual, r_rs, h_out, h_rs, w, y, y_rs, D, eps)
+             : launch_rms<_Float16>(rows, st, x, x_rs, residual, r_rs, h_out, h_rs, w, y, y_rs, D, eps);
 }
 
 int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads, int d, const void* cos_t,
-                      const void* sin_t, int64_t tab_rs, const int64_t* pos, cram_stream_t stream) {
+                      const void* sin_t, int64_t tab_rs, const int64_t* pos, int dtype, cram_stream_t stream) {
   if (!qkv || !cos_t || !sin_t || rows < 0 || heads <= 0 || T <= 0) return CRAM_ERR_INVALID_ARG;
+  if (!dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (rows == 0) return CRAM_OK;
   if ((d & 15) || !m8(row_stride) || !m8(tab_rs) || !al16(qkv) || !al16(cos_t) || !al16(sin_t))
     return CRAM_ERR_ALIGNMENT;
   const int64_t total = (int64_t)rows * heads * (d / 16);
   if (total >= (1ll << 31)) return CRAM_ERR_INVALID_ARG;
-  hipLaunchKernelGGL(rope_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     (__bf16*)qkv, row_stride, rows, T, heads, d, (const __bf16*)cos_t, (const __bf16*)sin_t,
-                     tab_rs, pos);
+  const dim3 g((unsigned)((total + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRAM_DTYPE_BF16)
+    hipLaunchKernelGGL(rope_kernel<__bf16>, g, dim3(256), 0, st, (__bf16*)qkv, row_stride, rows, T, heads, d,
+                       (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos);
+  else
+    hipLaunchKernelGGL(rope_kernel<_Float16>, g, dim3(256), 0, st, (_Float16*)qkv, row_stride, rows, T, heads, d,
+                       (const _Float16*)cos_t, (const _Float16*)sin_t, tab_rs, pos);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 
-int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, cram_stream_t stream) {
+int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, int dtype,
+                  cram_stream_t stream) {
   if (!gu || !y || rows < 0 || F <= 0) return CRAM_ERR_INVALID_ARG;
+  if (!dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (rows == 0) return CRAM_OK;
   if ((F & 7) || !m8(gu_rs) || !m8(y_rs) || !al16(gu) || !al16(y)) return CRAM_ERR_ALIGNMENT;
   const int64_t total = (int64_t)rows * (F / 8);
   if (total >= (1ll << 31)) return CRAM_ERR_INVALID_ARG;
-  hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     (const __bf16*)gu, gu_rs, (__bf16*)y, y_rs, rows, F);
+  const dim3 g((unsigned)((total + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRAM_DTYPE_BF16)
+    hipLaunchKernelGGL(silu_mul_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)gu, gu_rs, (__bf16*)y, y_rs,
+                       rows, F);
+  else
+    hipLaunchKernelGGL(silu_mul_kernel<_Float16>, g, dim3(256), 0, st, (const _Float16*)gu, gu_rs, (_Float16*)y,
+                       y_rs, rows, F);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 

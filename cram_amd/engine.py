@@ -7,7 +7,7 @@ same shapes for throughput runs) with:
   * fused QKV and gate/up projections (one hipBLASLt GEMM each, via torch),
   * credibility-biased attention from libcram_attn (prefill MFMA kernel,
     decode split-S kernel) reading q/k/v straight out of the QKV buffer,
-  * a static per-batch KV cache ([L][B][Hkv][S_max][d], bf16) and a decode
+  * a static per-batch KV cache ([L][B][Hkv][S_max][d], model dtype) and a decode
     step whose attention reads per-row lengths from device memory, so a whole
     greedy step can be captured in one hipGraph and replayed,
   * answer-token logits by the fp32 gather kernel instead of the full-vocab
@@ -66,6 +66,11 @@ class ModelSpec:
     @staticmethod
     def qwen2_7b() -> "ModelSpec":
         return ModelSpec(28, 3584, 28, 4, 128, 18944, 152064, 1e-6, True, "qwen2")
+
+    # the reference's default model (re_weighting.py:22 model_name="Llama-2-13b-chat-hf"): MHA, fp16 checkpoint
+    @staticmethod
+    def llama2_13b() -> "ModelSpec":
+        return ModelSpec(40, 5120, 40, 40, 128, 13824, 32000, 1e-5, False, "llama")
 
     def layer_flops(self, T: int) -> float:
         """GEMM flops of one decoder layer over T tokens (2 * params * T)."""
@@ -175,7 +180,7 @@ class CrAMEngine:
         return ops.rmsnorm(delta, w, self.spec.eps, residual=h if h.is_contiguous() else h.contiguous())
 
     def rope_tables(self, P: int):
-        """bf16 cos, sin [P, d] for positions 0..P-1 (LlamaRotaryEmbedding.forward arithmetic)."""
+        """cos, sin (model dtype) [P, d] for positions 0..P-1 (LlamaRotaryEmbedding.forward arithmetic)."""
         freqs = torch.arange(P, device=self.device, dtype=torch.float32)[:, None] * self.inv_freq[None, :]
         emb = torch.cat((freqs, freqs), dim=-1)
         return (emb.cos() * self.attn_scaling).to(self.dtype), (emb.sin() * self.attn_scaling).to(self.dtype)
@@ -283,9 +288,9 @@ class CrAMEngine:
         h = self.forward_hidden(ids, cb, out_rows=last)
         return ops.linear(h, self.lm_head)
 
-    def answer_logits(self, hidden: torch.Tensor, ids: torch.Tensor, round_bf16: bool = False) -> torch.Tensor:
-        """hidden [n, D] bf16, ids int32 [n] -> fp32 [n] (HIP gather-dot)."""
-        return ops.answer_logits(hidden.contiguous(), self.lm_head, ids, round_bf16=round_bf16)
+    def answer_logits(self, hidden: torch.Tensor, ids: torch.Tensor, round_logits: bool = False) -> torch.Tensor:
+        """hidden [n, D] (model dtype), ids int32 [n] -> fp32 [n] (HIP gather-dot)."""
+        return ops.answer_logits(hidden.contiguous(), self.lm_head, ids, round_logits=round_logits)
 
     # ------------------------------------------------------------------ batched greedy decode
     @torch.no_grad()

@@ -78,9 +78,22 @@ def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
-def _check_bf16(name: str, t: torch.Tensor, ndim: int) -> None:
-    if t.dtype != torch.bfloat16:
-        raise TypeError(f"{name} must be bfloat16, got {t.dtype}")
+# element types of the kernels (include/cram_attn.h CRAM_DTYPE_*): the model dtype the reference loads with
+# dtype="auto" (bf16 for Llama-3 / Qwen2, fp16 for Llama-2 checkpoints)
+DTYPES = {torch.bfloat16: 0, torch.float16: 1}
+
+
+def _dt(t: torch.Tensor) -> int:
+    try:
+        return DTYPES[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported element type {t.dtype}: the kernels take bfloat16 or float16") from None
+
+
+def _check16(name: str, t: torch.Tensor, ndim: int, like: Optional[torch.Tensor] = None) -> None:
+    _dt(t)
+    if like is not None and t.dtype != like.dtype:
+        raise TypeError(f"{name} is {t.dtype} but the other operands are {like.dtype}")
     if t.dim() != ndim:
         raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
     if t.stride(-1) != 1:
@@ -110,9 +123,9 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: fl
     Returns ``out`` [B, Tq, Hq, d] (the layout transformers' attention
     interface returns); query i sits at position ``q_pos0 + i`` (default S - Tq).
     """
-    _check_bf16("q", q, 4)
-    _check_bf16("k", k, 4)
-    _check_bf16("v", v, 4)
+    _check16("q", q, 4)
+    _check16("k", k, 4, q)
+    _check16("v", v, 4, q)
     B, Hq, Tq, d = q.shape
     _, Hkv, S, _ = k.shape
     if k.shape[0] != B or v.shape != k.shape or k.shape[3] != d:
@@ -122,7 +135,7 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: fl
     if out is None:
         out = torch.empty((B, Tq, Hq, d), dtype=q.dtype, device=q.device)
     elif out.shape != (B, Tq, Hq, d) or out.dtype != q.dtype or out.stride(-1) != 1:
-        raise ValueError("out must be bf16 [B, Tq, Hq, d] with a contiguous last dim")
+        raise ValueError("out must be [B, Tq, Hq, d] of q's dtype with a contiguous last dim")
     bp, bsb, ep, esb, W = _bias_args(bias, enable, B, Hq, W)
     lib = _lib.load()
     ev = TIMER.record("cram_prefill", *prefill_work(B, Hq, Hkv, Tq, S, d, q_pos0), q.device) if TIMER.enabled else None
@@ -132,7 +145,7 @@ def attn_prefill(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: fl
         v.data_ptr(), v.stride(0), v.stride(1), v.stride(2),
         out.data_ptr(), out.stride(0), out.stride(2), out.stride(1),
         B, Hq, Hkv, Tq, S, d, int(q_pos0), float(scale),
-        bp, bsb, ep, esb, W, _stream(q.device))
+        bp, bsb, ep, esb, W, _dt(q), _stream(q.device))
     _lib.check(code, "cram_attn_prefill")
     if ev is not None:
         ev.record(torch.cuda.current_stream(q.device))
@@ -144,9 +157,9 @@ def attn_prefill_varlen(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_se
                         W: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Packed causal attention: q [total, Hq, d], k/v [total, Hkv, d] (token-major, any token stride),
     sequence b = tokens [cu[b], cu[b+1]).  Returns out [total, Hq, d]."""
-    _check_bf16("q", q, 3)
-    _check_bf16("k", k, 3)
-    _check_bf16("v", v, 3)
+    _check16("q", q, 3)
+    _check16("k", k, 3, q)
+    _check16("v", v, 3, q)
     total, Hq, d = q.shape
     Hkv = k.shape[1]
     B = cu_seqlens.numel() - 1
@@ -160,7 +173,8 @@ def attn_prefill_varlen(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_se
     code = _lib.load().cram_attn_prefill_varlen(
         q.data_ptr(), q.stride(1), q.stride(0), k.data_ptr(), k.stride(1), k.stride(0),
         v.data_ptr(), v.stride(1), v.stride(0), out.data_ptr(), out.stride(1), out.stride(0),
-        cu_seqlens.data_ptr(), B, int(max_len), Hq, Hkv, d, float(scale), bp, bsb, ep, esb, W, _stream(q.device))
+        cu_seqlens.data_ptr(), B, int(max_len), Hq, Hkv, d, float(scale), bp, bsb, ep, esb, W, _dt(q),
+        _stream(q.device))
     _lib.check(code, "cram_attn_prefill_varlen")
     if ev is not None:
         ev.record(torch.cuda.current_stream(q.device))
@@ -181,9 +195,9 @@ def attn_decode(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: flo
     (default: all S_max).  ``num_splits`` > 1 needs ``workspace`` (uint8, at
     least ``decode_workspace_bytes`` bytes).
     """
-    _check_bf16("q", q, 3)
-    _check_bf16("k", k, 4)
-    _check_bf16("v", v, 4)
+    _check16("q", q, 3)
+    _check16("k", k, 4, q)
+    _check16("v", v, 4, q)
     B, Hq, d = q.shape
     _, Hkv, S, _ = k.shape
     if k.shape[0] != B or v.shape != k.shape or k.shape[3] != d:
@@ -206,16 +220,17 @@ def attn_decode(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: flo
         v.data_ptr(), v.stride(0), v.stride(1), v.stride(2),
         out.data_ptr(), out.stride(0), out.stride(1),
         B, Hq, Hkv, S, _ptr(seq_lens), d, float(scale),
-        bp, bsb, ep, esb, W, int(num_splits), ws_ptr, ws_bytes, _stream(q.device))
+        bp, bsb, ep, esb, W, int(num_splits), ws_ptr, ws_bytes, _dt(q), _stream(q.device))
     _lib.check(code, "cram_attn_decode")
     return out
 
 
-def answer_logits(hidden: torch.Tensor, w_lm: torch.Tensor, ids: torch.Tensor, *, round_bf16: bool = False,
+def answer_logits(hidden: torch.Tensor, w_lm: torch.Tensor, ids: torch.Tensor, *, round_logits: bool = False,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """out[i] = <hidden[i], w_lm[ids[i]]> in fp32.  hidden [n, D] bf16, w_lm [V, D] bf16, ids int32 [n]."""
-    _check_bf16("hidden", hidden, 2)
-    _check_bf16("w_lm", w_lm, 2)
+    """out[i] = <hidden[i], w_lm[ids[i]]> in fp32, rounded to the model dtype first if ``round_logits``.
+    hidden [n, D], w_lm [V, D] (bf16 or fp16, same dtype), ids int32 [n]."""
+    _check16("hidden", hidden, 2)
+    _check16("w_lm", w_lm, 2, hidden)
     n, D = hidden.shape
     if w_lm.shape[1] != D or ids.dtype != torch.int32 or ids.shape != (n,):
         raise ValueError("answer_logits: hidden [n, D], w_lm [V, D], ids int32 [n]")
@@ -223,7 +238,7 @@ def answer_logits(hidden: torch.Tensor, w_lm: torch.Tensor, ids: torch.Tensor, *
         out = torch.empty(n, dtype=torch.float32, device=hidden.device)
     lib = _lib.load()
     code = lib.cram_answer_logits(hidden.data_ptr(), hidden.stride(0), w_lm.data_ptr(), w_lm.stride(0),
-                                  ids.data_ptr(), n, D, int(bool(round_bf16)), out.data_ptr(),
+                                  ids.data_ptr(), n, D, int(bool(round_logits)), out.data_ptr(), _dt(hidden),
                                   _stream(hidden.device))
     _lib.check(code, "cram_answer_logits")
     return out
@@ -244,7 +259,8 @@ def _rows2d(t: torch.Tensor, name: str) -> torch.Tensor:
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
             h_out: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
     """LlamaRMSNorm(x [+ residual]).  Returns y, or (h, y) when residual is given (h = x + residual)."""
-    _check_bf16("w", w, 1)
+    _check16("w", w, 1)
+    _check16("x", x, x.dim(), w)
     x2 = _rows2d(x, "x")
     rows, D = x2.shape
     if out is None:
@@ -258,7 +274,7 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[tor
         h2 = _rows2d(h_out, "h_out")
     code = _lib.load().cram_rmsnorm(x2.data_ptr(), x2.stride(0), _ptr(r2), r2.stride(0) if r2 is not None else 0,
                                     _ptr(h2), h2.stride(0) if h2 is not None else 0, w.data_ptr(), y2.data_ptr(),
-                                    y2.stride(0), rows, D, float(eps), _stream(x.device))
+                                    y2.stride(0), rows, D, float(eps), _dt(x), _stream(x.device))
     _lib.check(code, "cram_rmsnorm")
     return (h_out, out) if residual is not None else out
 
@@ -267,23 +283,26 @@ def rope_inplace(qkv: torch.Tensor, heads: int, head_dim: int, cos: torch.Tensor
                  pos: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Rotate the first `heads` heads of every row of the fused QKV buffer in place (apply_rotary_pos_emb)."""
     y2 = _rows2d(qkv, "qkv")
-    if cos.dtype != torch.bfloat16 or cos.shape != sin.shape or cos.stride(-1) != 1:
-        raise ValueError("cos/sin must be bf16 [P, d] tables")
+    _dt(qkv)
+    if cos.dtype != qkv.dtype or sin.dtype != qkv.dtype or cos.shape != sin.shape or cos.stride(-1) != 1:
+        raise ValueError("cos/sin must be [P, d] tables of the QKV buffer's dtype")
     if pos is not None and (pos.dtype != torch.int64 or pos.numel() != y2.shape[0]):
         raise ValueError("pos must be int64 with one entry per row")
     code = _lib.load().cram_rope_inplace(y2.data_ptr(), y2.stride(0), y2.shape[0], int(T), int(heads), int(head_dim),
-                                         cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), _stream(qkv.device))
+                                         cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), _dt(qkv),
+                                         _stream(qkv.device))
     _lib.check(code, "cram_rope_inplace")
     return qkv
 
 
 def silu_mul(gu: torch.Tensor, F: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """bf16(silu(gu[..., :F])) * gu[..., F:2F] (LlamaMLP activation)."""
+    """rnd(silu(gu[..., :F])) * gu[..., F:2F] (LlamaMLP activation), bf16 or fp16."""
+    _dt(gu)
     g2 = _rows2d(gu, "gu")
     if out is None:
         out = torch.empty(gu.shape[:-1] + (F,), dtype=gu.dtype, device=gu.device)
     y2 = _rows2d(out, "out")
     code = _lib.load().cram_silu_mul(g2.data_ptr(), g2.stride(0), y2.data_ptr(), y2.stride(0), g2.shape[0], int(F),
-                                     _stream(gu.device))
+                                     _dt(gu), _stream(gu.device))
     _lib.check(code, "cram_silu_mul")
     return out

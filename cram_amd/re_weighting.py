@@ -184,7 +184,7 @@ class Find_Best_Heads(Re_Weighting_Strategy):
 
     @torch.no_grad()
     def cal_logits_tensor(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
-                          wrong_answer: str = "my name is", round_bf16_logits: bool = False) -> torch.Tensor:
+                          wrong_answer: str = "my name is", round_logits: bool = False) -> torch.Tensor:
         """IE [L, H] fp32 on the device (no host sync)."""
         ans = self.answer_ids(wrong_answer)
         model_inputs, w = self.decode_with_special_attention(question=question, paras=paras, scores=scores,
@@ -193,13 +193,13 @@ class Find_Best_Heads(Re_Weighting_Strategy):
         if ans.numel() == 0:   # the reference sums an empty selection: IE == 0 everywhere
             return torch.zeros((L, H), dtype=torch.float32, device=self.device)
         if not CrAMEngine.supports(self.model):
-            return self._ie_per_head(model_inputs["input_ids"], w, ans, round_bf16_logits)
+            return self._ie_per_head(model_inputs["input_ids"], w, ans, round_logits)
         return _sweep.ie_question(self.engine, model_inputs["input_ids"][0], w[0].cpu(), ans,
-                                  round_bf16_logits=round_bf16_logits)
+                                  round_logits=round_logits)
 
     @torch.no_grad()
     def _ie_per_head(self, ids: torch.Tensor, w16: torch.Tensor, ans: torch.Tensor,
-                     round_bf16_logits: bool) -> torch.Tensor:
+                     round_logits: bool) -> torch.Tensor:
         """The reference algorithm itself (re_weighting.py:157-175: one un-hooked forward, then one forward per
         (layer, head) with only that head re-weighted) on the transformers model with the cram_hip kernels, for
         architectures the batched engine does not implement (GPT-2).  Answer logits in fp32 like the sweep."""
@@ -211,7 +211,7 @@ class Find_Best_Heads(Re_Weighting_Strategy):
         def total(cb):
             with _attn.reweighting(self.model, cb):
                 hid = self.model.base_model(input_ids=ids).last_hidden_state[0, -n:]
-            return self._answer_logits(hid, w_lm, ans_d, round_bf16_logits).sum()
+            return self._answer_logits(hid, w_lm, ans_d, round_logits).sum()
 
         ori = total(None)
         out = torch.empty((L, H), dtype=torch.float32, device=self.device)
@@ -221,19 +221,19 @@ class Find_Best_Heads(Re_Weighting_Strategy):
         return out
 
     @staticmethod
-    def _answer_logits(hidden, w_lm, ids, round_bf16):
+    def _answer_logits(hidden, w_lm, ids, round_logits):
         from . import ops
-        return ops.answer_logits(hidden.to(torch.bfloat16).contiguous(), w_lm.to(torch.bfloat16), ids,
-                                 round_bf16=round_bf16)
+        dt = hidden.dtype if hidden.dtype in ops.DTYPES else torch.bfloat16    # fp32 models (GPT-2): bf16 operands
+        return ops.answer_logits(hidden.to(dt).contiguous(), w_lm.to(dt), ids, round_logits=round_logits)
 
     @torch.no_grad()
     def cal_logits_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
-                         wrong_answers: List[str], round_bf16_logits: bool = False) -> torch.Tensor:
+                         wrong_answers: List[str], round_logits: bool = False) -> torch.Tensor:
         """IE of many questions as one device tensor [Nq, L, H] fp32 (the sweep's batched form)."""
         out = torch.empty((len(questions), self.model_num_hidden_layers, self.model_num_attention_heads),
                           dtype=torch.float32, device=self.device)
         for i, (q, p, s, a) in enumerate(zip(questions, paras_list, scores_list, wrong_answers)):
-            out[i] = self.cal_logits_tensor(q, p, s, "", a, round_bf16_logits)
+            out[i] = self.cal_logits_tensor(q, p, s, "", a, round_logits)
         return out
 
     def cal_logits(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",

@@ -132,7 +132,7 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
 
 @torch.no_grad()
 def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answer_ids: torch.Tensor,
-                layers=None, round_bf16_logits: bool = False, skip_prefix: bool = True) -> torch.Tensor:
+                layers=None, round_logits: bool = False, skip_prefix: bool = True) -> torch.Tensor:
     """IE [len(layers), H] (fp32, device) for one question — the value cal_logits returns.
 
     ids [T'] (prompt + answer), weight16 fp16 [T'] (sweep scores), answer_ids [n]
@@ -152,7 +152,7 @@ def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answ
     p0 = first_biased_row(cb.bias, cb.W) if skip_prefix else 0
     for i, l in enumerate(layers):
         hv = layer_variants(eng, qc, l, cb.bias, cb.W, n, p0=p0)       # [H+1, n, D]
-        sums = eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_bf16_logits).view(H1, n).sum(1)
+        sums = eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_logits).view(H1, n).sum(1)
         out[i] = sums[-1] - sums[:-1]                                   # ori - cur
     return out
 

@@ -62,7 +62,7 @@ int main(void) {
                              dk, (int64_t)Hkv * T * d, (int64_t)T * d, d,
                              dv, (int64_t)Hkv * T * d, (int64_t)T * d, d,
                              dout, (int64_t)T * Hq * d, d, (int64_t)Hq * d,
-                             B, Hq, Hkv, T, T, d, 0, scale, dbias, T, den, Hq, W, NULL);
+                             B, Hq, Hkv, T, T, d, 0, scale, dbias, T, den, Hq, W, CRAM_DTYPE_BF16, NULL);
   if (rc != CRAM_OK) { fprintf(stderr, "cram_attn_prefill: %s\n", cram_strerror(rc)); return 3; }
   CHECK(hipDeviceSynchronize());
   CHECK(hipMemcpy(ho, dout, nq * 2, hipMemcpyDeviceToHost));
@@ -91,7 +91,7 @@ int main(void) {
       }
   /* the error path: an unsupported head dim is rejected before any launch */
   rc = cram_attn_prefill(dq, 0, 0, 0, dk, 0, 0, 0, dv, 0, 0, 0, dout, 0, 0, 0,
-                         1, 1, 1, 1, 1, 96, 0, 1.0f, NULL, 0, NULL, 0, 0, NULL);
+                         1, 1, 1, 1, 1, 96, 0, 1.0f, NULL, 0, NULL, 0, 0, CRAM_DTYPE_BF16, NULL);
   printf("abi %d: prefill B=%d Hq=%d Hkv=%d T=%d d=%d max|err|=%.3e; d=96 -> %d (%s)\n", cram_abi_version(), B, Hq,
          Hkv, T, d, max_err, rc, cram_strerror(rc));
   hipFree(dq); hipFree(dk); hipFree(dv); hipFree(dout); hipFree(dbias); hipFree(den);

@@ -6,7 +6,7 @@
  * dense attention mask of every selected (layer, head):
  *
  *   /root/reference/utils/re_weighting.py:36-61   Re_Weighting_Strategy.edit_attention_mask
- *       mask[0,h,i,j] = bf16(log_fp16(w_j))  for causal-allowed (i, j), j < W, h in head_idx
+ *       mask[0,h,i,j] = dtype(log_fp16(w_j))  for causal-allowed (i, j), j < W, h in head_idx
  *   /root/reference/utils/re_weighting.py:118-124 hook registration (generate path)
  *   /root/reference/utils/re_weighting.py:163-168 hook registration (IE sweep path)
  *
@@ -19,10 +19,13 @@
  * Conventions
  *   - all tensor pointers are DEVICE pointers owned by the caller; no entry
  *     point allocates, frees or synchronises;
- *   - q/k/v/o are bf16, last dimension contiguous, every stride given in
- *     ELEMENTS and a multiple of 8, every base pointer 16-byte aligned;
+ *   - q/k/v/o (and every other 16-bit tensor) are bf16 or fp16, named by the
+ *     `dtype` argument (CRAM_DTYPE_*: the model's torch_dtype, which the
+ *     reference loads with dtype="auto" -> bf16 for Llama-3 / Qwen2, fp16 for
+ *     Llama-2, re_weighting.py:22); last dimension contiguous, every stride
+ *     given in ELEMENTS and a multiple of 8, every base pointer 16-byte aligned;
  *   - bias is fp32 [B][bias_sb] in natural-log units (the hook's
- *     bf16(log_fp16(w)) already widened to fp32); enable is uint8 [B][en_sb];
+ *     dtype(log_fp16(w)) already widened to fp32); enable is uint8 [B][en_sb];
  *     a NULL bias or NULL enable means "no re-weighting" (plain causal);
  *   - work is enqueued on `stream` (a hipStream_t; NULL = default stream);
  *   - every entry point returns CRAM_OK (0) or a negative CRAM_ERR_* code and
@@ -40,10 +43,15 @@ extern "C" {
 
 #define CRAM_OK 0
 #define CRAM_ERR_INVALID_ARG -1   /* null pointer, non-positive size, Hq % Hkv != 0 ... */
-#define CRAM_ERR_UNSUPPORTED -2   /* head dim not in {64,128}, GQA group size not supported */
+#define CRAM_ERR_UNSUPPORTED -2   /* head dim not in {64,128}, GQA group size or dtype not supported */
 #define CRAM_ERR_ALIGNMENT -3     /* stride not a multiple of 8 elements / pointer not 16-B aligned */
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
+
+#define CRAM_ABI_VERSION 2        /* 2: dtype argument on every tensor entry point */
+
+#define CRAM_DTYPE_BF16 0
+#define CRAM_DTYPE_F16 1
 
 typedef void* cram_stream_t; /* hipStream_t */
 
@@ -67,7 +75,7 @@ int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st,
                       void* o, int64_t o_sb, int64_t o_sh, int64_t o_st,
                       int B, int Hq, int Hkv, int Tq, int S, int d, int q_pos0, float scale,
                       const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
-                      cram_stream_t stream);
+                      int dtype, cram_stream_t stream);
 
 /*
  * Packed variable-length prefill (batched reweighted decode: many prompts in one GEMM pass).
@@ -79,7 +87,7 @@ int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const vo
                              const void* v, int64_t v_sh, int64_t v_st, void* o, int64_t o_sh, int64_t o_st,
                              const int32_t* cu_seqlens, int B, int max_len, int Hq, int Hkv, int d, float scale,
                              const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
-                             cram_stream_t stream);
+                             int dtype, cram_stream_t stream);
 
 /*
  * Single-token decode attention (replaces the hooked SDPA call for q_len == 1;
@@ -99,36 +107,40 @@ int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh,
                      int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d, float scale,
                      const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
                      int num_splits, void* workspace, size_t workspace_bytes,
-                     cram_stream_t stream);
+                     int dtype, cram_stream_t stream);
 
 /*
  * Answer-token logits (replaces the full-vocab lm_head + gather of
  * re_weighting.py:159-160,169-170):  out[i] = sum_d hidden[i][d] * w_lm[ids[i]][d]
- * in fp32; round_bf16 != 0 rounds each logit to bf16 first (transformers 5.15 bf16 logits).
- *   hidden : bf16 [n][D] row stride h_rs;  w_lm : bf16 [V][D] row stride w_rs;  ids : int32 [n]
+ * in fp32; round_logits != 0 rounds each logit to `dtype` first (transformers 5.15 returns
+ * logits in the model dtype).
+ *   hidden : [n][D] row stride h_rs;  w_lm : [V][D] row stride w_rs;  ids : int32 [n]
  */
 int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64_t w_rs,
-                       const int32_t* ids, int n, int D, int round_bf16, float* out,
-                       cram_stream_t stream);
+                       const int32_t* ids, int n, int D, int round_logits, float* out,
+                       int dtype, cram_stream_t stream);
 
 /*
- * Fused elementwise kernels of the engine (cram_fused.hip), bf16, rows of 16-byte aligned vectors.
+ * Fused elementwise kernels of the engine (cram_fused.hip), bf16 or fp16 (`dtype`), rows of 16-byte
+ * aligned vectors; below, rnd() rounds to that dtype.
  * They keep transformers' rounding points (LlamaRMSNorm, apply_rotary_pos_emb, LlamaMLP), i.e. the
  * arithmetic the reference's hooked model runs between its GEMMs (re_weighting.py:127 -> generate,
  * :159/:169 -> model forward).
  *
- * cram_rmsnorm       y = bf16(w * bf16(h * rsqrt(mean(h^2) + eps))) per row; if residual != NULL then
- *                    h = bf16(x + residual) is also written to h_out, else h = x.
+ * cram_rmsnorm       y = rnd(w * rnd(h * rsqrt(mean(h^2) + eps))) per row; if residual != NULL then
+ *                    h = rnd(x + residual) is also written to h_out, else h = x.
  * cram_rope_inplace  rotates the first `heads` heads (q then k) of every row of a fused QKV buffer in
  *                    place; row r uses position pos[r] (int64) or r % T when pos == NULL; cos/sin are
- *                    bf16 [P][d] tables (row stride tab_rs).
- * cram_silu_mul      y[r, :F] = bf16(bf16(silu(gu[r, :F])) * gu[r, F:2F])
+ *                    [P][d] tables of the same dtype (row stride tab_rs).
+ * cram_silu_mul      y[r, :F] = rnd(rnd(silu(gu[r, :F])) * gu[r, F:2F])
  */
 int cram_rmsnorm(const void* x, int64_t x_rs, const void* residual, int64_t r_rs, void* h_out, int64_t h_rs,
-                 const void* w, void* y, int64_t y_rs, int rows, int D, float eps, cram_stream_t stream);
+                 const void* w, void* y, int64_t y_rs, int rows, int D, float eps, int dtype,
+                 cram_stream_t stream);
 int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads, int d, const void* cos_t,
-                      const void* sin_t, int64_t tab_rs, const int64_t* pos, cram_stream_t stream);
-int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, cram_stream_t stream);
+                      const void* sin_t, int64_t tab_rs, const int64_t* pos, int dtype, cram_stream_t stream);
+int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, int dtype,
+                  cram_stream_t stream);
 
 /*
  * Host-side prompt -> credibility weights (cram_spans.cpp; no device, no stream), batched over B prompts.

@@ -17,7 +17,7 @@ from . import hook_ref
 
 
 def hf_model_from_engine(eng, rope_theta: float = 500000.0):
-    """A transformers LlamaForCausalLM on the CPU holding the engine's weights (bf16)."""
+    """A transformers LlamaForCausalLM on the CPU holding the engine's weights (in the engine's dtype)."""
     from transformers import LlamaConfig, LlamaForCausalLM
     sp = eng.spec
     cfg = LlamaConfig(vocab_size=sp.vocab, hidden_size=sp.hidden, intermediate_size=sp.intermediate,
@@ -26,7 +26,7 @@ def hf_model_from_engine(eng, rope_theta: float = 500000.0):
                       rope_theta=rope_theta, max_position_embeddings=8192, tie_word_embeddings=False)
     cfg._attn_implementation = "sdpa"
     prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.bfloat16)
+    torch.set_default_dtype(eng.dtype)
     try:
         with torch.device("meta"):
             model = LlamaForCausalLM(cfg)

@@ -70,10 +70,10 @@ def attn_prefill_varlen(q, k, v, cu_seqlens, max_len, *, scale, bias=None, enabl
     return res
 
 
-def answer_logits(hidden, w_lm, ids, *, round_bf16=False, out=None):
+def answer_logits(hidden, w_lm, ids, *, round_logits=False, out=None):
     r = (hidden.float() * w_lm[ids.long()].float()).sum(-1)
-    if round_bf16:
-        r = r.to(torch.bfloat16).float()
+    if round_logits:
+        r = r.to(hidden.dtype).float()
     return r
 
 

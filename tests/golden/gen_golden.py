@@ -17,6 +17,9 @@ Outputs (data only) in tests/golden/:
   tiny_ie_f32.json.gz G4' cal_logits on the float32 copy of the same weights (IE ground truth)
   generate.json.gz  G5  run_RAG_with_attention_weighting outputs + greedy ids + hooked last-row logits
   logprobs.json.gz  G6  re-weighted answer-token log-probabilities through the reference hook (bf16 + fp32 copies)
+  llama2_*.json.gz  G4/G4'/G5/G6 for the fp16 MHA Llama-2 stand-in (`python gen_golden.py llama2`): the reference's
+                    default model family, loaded as fp16 by torch_dtype="auto"; its "bf16" IE variant holds the
+                    model-dtype (fp16) logits
 """
 import contextlib
 import gzip
@@ -146,9 +149,9 @@ def fp32_lm_head(model):
     return model.lm_head.register_forward_hook(hook)
 
 
-def gen_ie(rw):
+def gen_ie(rw, kinds=(("llama3", 6), ("qwen2", 3)), out="tiny_ie.json.gz"):
     res = []
-    for kind, nq in (("llama3", 6), ("qwen2", 3)):
+    for kind, nq in kinds:
         path = tm.save_model(kind, MODEL_ROOT)
         with cuda_to_cpu():
             fbh = rw.Find_Best_Heads(model_name=path)
@@ -171,14 +174,14 @@ def gen_ie(rw):
             if h is not None:
                 h.remove()
         del fbh
-    with gzip.open(os.path.join(OUT, "tiny_ie.json.gz"), "wt", encoding="utf-8") as f:
+    with gzip.open(os.path.join(OUT, out), "wt", encoding="utf-8") as f:
         json.dump(res, f)
 
 
-def gen_ie_f32(rw):
+def gen_ie_f32(rw, kinds=(("llama3", 6), ("qwen2", 3)), out="tiny_ie_f32.json.gz"):
     """The reference's cal_logits on the float32 copy of the tiny models: the IE ground truth."""
     res = []
-    for kind, nq in (("llama3", 6), ("qwen2", 3)):
+    for kind, nq in kinds:
         path = tm.save_model(kind, MODEL_ROOT, fp32=True)
         with cuda_to_cpu():
             fbh = rw.Find_Best_Heads(model_name=path)
@@ -191,14 +194,15 @@ def gen_ie_f32(rw):
             res.append({"kind": kind, "variant": "f32model", "idx": i, "ie": grid})
             print(kind, "f32model", i, float(np.min(grid)), float(np.max(grid)))
         del fbh
-    with gzip.open(os.path.join(OUT, "tiny_ie_f32.json.gz"), "wt", encoding="utf-8") as f:
+    with gzip.open(os.path.join(OUT, out), "wt", encoding="utf-8") as f:
         json.dump(res, f)
 
 
-def gen_generate(rw):
+def gen_generate(rw, cases=(("llama3", {0: [1], 1: [0, 3], 3: [2]}), ("llama3", {}), ("qwen2", {1: [0]})),
+                 out="generate.json.gz"):
     res = []
     recs = load_data("nq")[:4]
-    for kind, heads in (("llama3", {0: [1], 1: [0, 3], 3: [2]}), ("llama3", {}), ("qwen2", {1: [0]})):
+    for kind, heads in cases:
         path = tm.save_model(kind, MODEL_ROOT)
         with cuda_to_cpu():
             obj = rw.Re_Weighting_Strategy(model_name=path, layers_to_be_modified=dict(heads), bad_words_ids=[])
@@ -222,18 +226,18 @@ def gen_generate(rw):
                         "prompt": prompt, "output": output, "ids": rec_ids["ids"],
                         "last_logits": rec_ids["last_logits"]})
             print(kind, heads, i, len(rec_ids["ids"]), repr(output[:60]))
-    with gzip.open(os.path.join(OUT, "generate.json.gz"), "wt", encoding="utf-8") as f:
+    with gzip.open(os.path.join(OUT, out), "wt", encoding="utf-8") as f:
         json.dump(res, f)
 
 
-def gen_logprobs(rw):
+def gen_logprobs(rw, kinds=("llama3", "qwen2"), out="logprobs.json.gz"):
     """Re-weighted teacher-forced answer log-probabilities through the reference's own hook
     (Re_Weighting_Strategy.edit_attention_mask registered exactly as re_weighting.py:119-123 does),
     for the bf16 tiny models and their float32 copies (the ground truth)."""
     from functools import partial
     res = []
     recs = load_data("nq")[:3]
-    for kind in ("llama3", "qwen2"):
+    for kind in kinds:
         for fp32 in (False, True):
             path = tm.save_model(kind, MODEL_ROOT, fp32=fp32)
             with cuda_to_cpu():
@@ -268,7 +272,7 @@ def gen_logprobs(rw):
                                     "ids": ids[0].tolist(), "logprobs": lp.tolist()})
                         print(kind, fp32, i, sname, hname, [round(x, 4) for x in lp.tolist()])
             del obj
-    with gzip.open(os.path.join(OUT, "logprobs.json.gz"), "wt", encoding="utf-8") as f:
+    with gzip.open(os.path.join(OUT, out), "wt", encoding="utf-8") as f:
         json.dump(res, f)
 
 
@@ -287,6 +291,11 @@ def main():
         gen_generate(rw)
     if "logprobs" in which:
         gen_logprobs(rw)
+    if "llama2" in which:
+        gen_ie(rw, (("llama2", 3),), "llama2_ie.json.gz")
+        gen_ie_f32(rw, (("llama2", 3),), "llama2_ie_f32.json.gz")
+        gen_generate(rw, (("llama2", {0: [1], 2: [0, 3]}), ("llama2", {})), "llama2_generate.json.gz")
+        gen_logprobs(rw, ("llama2",), "llama2_logprobs.json.gz")
 
 
 if __name__ == "__main__":

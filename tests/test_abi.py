@@ -29,7 +29,7 @@ def test_library_builds_loads_and_exports_every_symbol():
         assert hasattr(lib, n), n
     assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
     L = _lib.load()
-    assert L.cram_abi_version() == 1
+    assert L.cram_abi_version() == _lib.ABI_VERSION == 2
     assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0
@@ -41,19 +41,23 @@ def test_argument_validation_without_gpu():
     L = _lib.load()
     # null pointers
     assert L.cram_attn_prefill(None, 0, 0, 0, None, 0, 0, 0, None, 0, 0, 0, None, 0, 0, 0,
-                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, None) == -1
+                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, 0, None) == -1
     # unsupported head dim (checked before alignment / launch)
     fake = 1 << 20
     assert L.cram_attn_prefill(fake, 0, 0, 0, fake, 0, 0, 0, fake, 0, 0, 0, fake, 0, 0, 0,
-                               1, 1, 1, 1, 1, 96, 0, 1.0, None, 0, None, 0, 0, None) == -2
+                               1, 1, 1, 1, 1, 96, 0, 1.0, None, 0, None, 0, 0, 0, None) == -2
+    # unsupported element type (only CRAM_DTYPE_BF16 = 0 and CRAM_DTYPE_F16 = 1)
+    assert L.cram_attn_prefill(fake, 0, 0, 0, fake, 0, 0, 0, fake, 0, 0, 0, fake, 0, 0, 0,
+                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, 2, None) == -2
+    assert L.cram_silu_mul(fake, 8, fake, 8, 1, 16, 7, None) == -2
     # misaligned stride
     assert L.cram_attn_prefill(fake, 8, 8, 12, fake, 0, 0, 8, fake, 0, 0, 8, fake, 0, 0, 8,
-                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, None) == -3
+                               1, 1, 1, 1, 1, 128, 0, 1.0, None, 0, None, 0, 0, 1, None) == -3
     # split decode without workspace
     assert L.cram_attn_decode(fake, 0, 0, fake, 0, 0, 8, fake, 0, 0, 8, fake, 0, 0,
-                              1, 1, 1, 4, None, 128, 1.0, None, 0, None, 0, 0, 4, None, 0, None) == -5
-    assert L.cram_rmsnorm(None, 0, None, 0, None, 0, None, None, 0, 1, 8, 1e-5, None) == -1
-    assert L.cram_silu_mul(fake, 8, fake, 8, 1, 12, None) == -3
+                              1, 1, 1, 4, None, 128, 1.0, None, 0, None, 0, 0, 4, None, 0, 0, None) == -5
+    assert L.cram_rmsnorm(None, 0, None, 0, None, 0, None, None, 0, 1, 8, 1e-5, 0, None) == -1
+    assert L.cram_silu_mul(fake, 8, fake, 8, 1, 12, 0, None) == -3
 
 
 def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):

@@ -25,10 +25,17 @@ from tests import tiny_models as tm
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
+def _gold(*names):
+    rows = []
+    for n in names:
+        with gzip.open(os.path.join(GOLD, n), "rt") as f:
+            rows += json.load(f)
+    return rows
+
+
 @pytest.fixture(scope="module")
 def ie_gold():
-    with gzip.open(os.path.join(GOLD, "tiny_ie.json.gz"), "rt") as f:
-        return json.load(f)
+    return _gold("tiny_ie.json.gz", "llama2_ie.json.gz")
 
 
 @pytest.fixture(scope="module")
@@ -42,7 +49,7 @@ def tiny(tmp_path_factory):
     from transformers import AutoModelForCausalLM, AutoTokenizer
     root = str(tmp_path_factory.mktemp("m"))
     out = {}
-    for k in ("llama3", "qwen2"):
+    for k in ("llama3", "qwen2", "llama2"):
         p = tm.save_model(k, root)
         out[k] = (p, AutoTokenizer.from_pretrained(p), AutoModelForCausalLM.from_pretrained(p, dtype="auto").eval())
     return out
@@ -55,7 +62,7 @@ def _question(tok, path, rec, answer=True):
     return enc["input_ids"], w
 
 
-@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+@pytest.mark.parametrize("kind", ["llama3", "qwen2", "llama2"])
 def test_engine_logits_match_transformers(tiny, nq, kind):
     path, tok, model = tiny[kind]
     ids, w = _question(tok, path, nq[0])
@@ -66,6 +73,7 @@ def test_engine_logits_match_transformers(tiny, nq, kind):
         ref = model(input_ids=ids).logits[0, -5:].float()
         truth = f32(input_ids=ids).logits[0, -5:].float()
     eng = CrAMEngine.from_hf(model)
+    assert eng.dtype == tm.dtype(kind)
     with cpu_ops.patched_ops():
         got = eng.logits(ids, last=5)[0].float()
     # bf16 noise floor: the engine must be as close to the fp32 model as transformers' own bf16 path is
@@ -87,16 +95,15 @@ def test_oracle_ie_matches_reference_bitwise(tiny, nq, ie_gold):
 
 @pytest.fixture(scope="module")
 def ie_truth():
-    with gzip.open(os.path.join(GOLD, "tiny_ie_f32.json.gz"), "rt") as f:
-        return json.load(f)
+    return _gold("tiny_ie_f32.json.gz", "llama2_ie_f32.json.gz")
 
 
 def ie_tolerance_check(ie, ref, truth):
     """Noise-floor criterion (written here once, used by the CPU and GPU suites).
 
-    ref   = the reference's own bf16 run (fp32 logits), truth = the reference run on the
-    float32 copy of the same weights.  The build must be as close to the truth as the
-    reference's bf16 arithmetic is:  mean|ie-truth| <= 2.5 mean|ref-truth| + 0.01 and
+    ref   = the reference's own bf16 (fp16 for Llama-2) run (fp32 logits), truth = the reference run on
+    the float32 copy of the same weights.  The build must be as close to the truth as the
+    reference's 16-bit arithmetic is:  mean|ie-truth| <= 2.5 mean|ref-truth| + 0.01 and
     max|ie-truth| <= 2.5 max|ref-truth| + 0.05; and every top-k set whose boundary gap in
     the truth exceeds 0.1 is identical for truth, ref and build.
     """
@@ -114,7 +121,7 @@ def ie_tolerance_check(ie, ref, truth):
             assert set(np.argsort(-ref.reshape(-1), kind="stable")[:k]) == top_t, k
 
 
-@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+@pytest.mark.parametrize("kind", ["llama3", "qwen2", "llama2"])
 def test_sweep_matches_reference_ie(tiny, nq, ie_gold, ie_truth, kind):
     """Head-batched layer-suffix sweep vs the reference's 1 + L*H hooked forwards."""
     path, tok, model = tiny[kind]

@@ -199,16 +199,14 @@ def test_native_span_rule_edge_cases():
     assert run([4, 8], [2], [9], [1.0])[0] == -1           # precedes every token
 
 
-@pytest.fixture(scope="module")
-def logprob_rows():
-    with gzip.open(os.path.join(GOLD, "logprobs.json.gz"), "rt", encoding="utf-8") as f:
-        return json.load(f)
-
-
-def test_oracle_answer_logprobs_bit_exact(logprob_rows, tmp_path_factory):
+@pytest.mark.parametrize("fixture", ["logprobs.json.gz", "llama2_logprobs.json.gz"])
+def test_oracle_answer_logprobs_bit_exact(fixture, tmp_path_factory):
     """G6: the oracle's hook restatement on the same transformers model reproduces the reference hook's
-    re-weighted answer log-probabilities exactly (bf16 and fp32 tiny models)."""
+    re-weighted answer log-probabilities exactly (bf16 Llama-3 / Qwen2, fp16 Llama-2 and their fp32 copies;
+    the Llama-2 rows also pin the raw-template prompt branch the reference's default model takes)."""
     from transformers import AutoModelForCausalLM, AutoTokenizer
+    with gzip.open(os.path.join(GOLD, fixture), "rt", encoding="utf-8") as f:
+        logprob_rows = json.load(f)
     root = str(tmp_path_factory.mktemp("tinylp"))
     with gzip.open(os.path.join(tm.REPO, "data", "nq_1000.json.gz"), "rt") as f:
         nq = json.load(f)

@@ -126,7 +126,7 @@ def test_answer_logits(gpu_device):
     out = ops.answer_logits(h.to(dev), w.to(dev), ids.to(dev))
     torch.cuda.synchronize()
     assert torch.allclose(out.double().cpu(), ref, atol=1e-3, rtol=1e-4)
-    out16 = ops.answer_logits(h.to(dev), w.to(dev), ids.to(dev), round_bf16=True)
+    out16 = ops.answer_logits(h.to(dev), w.to(dev), ids.to(dev), round_logits=True)
     assert torch.equal(out16.cpu(), out.cpu().to(torch.bfloat16).float())
 
 
