@@ -124,9 +124,16 @@ def main():
     ie = None
     if args.config == 3:
         n_q = (args.warmup + args.steps) * world
+        # weak scaling with equal per-GPU work at every N: questions are taken in order of closeness to the
+        # mean prompt length (characters of question + passages + wrong answer), step s on rank r gets the
+        # (s * N + r)-th, so the max-over-ranks step time does not grow with N from prompt-length spread alone
+        clen = [len(r["question"]) + sum(len(p) for p in r["ori_fake"] + r["reranked_dense_ctxs"])
+                + len(r["wrong_answer"]) for r in data]
+        mean_c = sum(clen) / len(clen)
+        pool = sorted(range(len(data)), key=lambda i: (abs(clen[i] - mean_c), i))
         work = []
         for s in range(args.warmup + args.steps):
-            qi = (s * world + rank) % len(data)
+            qi = pool[(s * world + rank) % len(pool)]
             rec = data[qi]
             _, enc, w, _ = spans.encode(tok, name, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
                                         [0, 1, 1, 1, 1], rec["wrong_answer"])
@@ -211,7 +218,10 @@ def main():
             B, encs = cap, encs[:cap]
         prompts = [ids.to(dev) for ids, _, _ in encs]
         ws = [w for _, w, _ in encs]
-        eng.generate(prompts[:2], ws[:2], heads, max_new_tokens=4)          # warm the graph path
+        # warm-up at the timed shape (the packed prefill's GEMM heuristics and buffers, the batch-B graph)
+        for _ in range(max(1, args.warmup)):
+            eng.generate(prompts, ws, heads, max_new_tokens=args.decode_tokens, eos_ids=(), use_graph=True,
+                         stop_on_eos=False)
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -289,7 +299,7 @@ def main():
                 "data": f"synthetic: random-init {name} weights; rebuilt NQ-1000 prompts via offline BPE tokenizer",
                 "config": {"workload": f"{name} Find_Best_Heads IE sweep, {L} layers x {H} heads per question, "
                                        "scores [0,1,1,1,1], 1 NQ question per GPU per step (config 3; decode = config 2)",
-                           "model": model, "questions_per_step": world, "mean_prompt_tokens": round(ie["mean_T"], 1),
+                           "model": model, "questions_per_step": world, "question_order": "nearest the mean NQ prompt length first, dealt round-robin to ranks", "mean_prompt_tokens": round(ie["mean_T"], 1),
                            "parallelism": f"dp{world} question-sharded + RCCL all-gather of IE"},
                 "roofline": roof,
                 "dominant_kernel": dom,

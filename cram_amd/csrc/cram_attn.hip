@@ -284,8 +284,15 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
       const char* base = smem + (t & 1) * C::STAGE;
       f32x16 sacc[C::NKB];
       const f32x16 zero16 = {};
+      // diagonal tile whose upper 32-key block lies past every query row of this wave (causal): that block's
+      // QK^T, softmax and PV are skipped (wave-uniform; its probabilities would all be exactly 0)
+      const bool hi_dead = C::NKB == 2 && key0 + 32 > wave_qpos_max;
 #pragma unroll
       for (int kb = 0; kb < C::NKB; ++kb) {
+        if (kb == 1 && hi_dead) {
+          sacc[kb] = zero16;
+          continue;
+        }
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
           const V8 a = *reinterpret_cast<const V8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
@@ -322,6 +329,7 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
         const int lim = min(qpos, S - 1) - key0;
 #pragma unroll
         for (int kb = 0; kb < C::NKB; ++kb) {
+          if (kb == 1 && hi_dead) continue;
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             f32x4 bv = {0.f, 0.f, 0.f, 0.f};
@@ -359,13 +367,15 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
       } else {
         const float sc = plain ? p.scale_log2 : 1.f;
 #pragma unroll
-        for (int kb = 0; kb < C::NKB; ++kb)
+        for (int kb = 0; kb < C::NKB; ++kb) {
+          if (kb == 1 && hi_dead) continue;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float pe = fast_exp2(__builtin_fmaf(sacc[kb][e], sc, -muse));
             sacc[kb][e] = pe;
             rs += pe;
           }
+        }
       }
       rs = half_sum(rs);
       CRAM_STAMP(2)
@@ -384,6 +394,7 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
       const char* vimg = base + C::V_OFF;
 #pragma unroll
       for (int kb = 0; kb < C::NKB; ++kb) {
+        if (kb == 1 && hi_dead) continue;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           V8 pb;

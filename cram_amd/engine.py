@@ -79,6 +79,8 @@ class ModelSpec:
 
 
 ROW_ALIGN = 256
+# packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where hipBLASLt already runs at full rate
+PREFILL_CHUNK_ROWS = 32768
 
 
 def padded_rows(M: int) -> int:
@@ -365,24 +367,42 @@ class DecodeSession:
             logits = logits.index_fill(-1, self.bad, float("-inf"))
         return torch.argmax(logits, dim=-1)
 
-    def prefill(self):
-        """All prompts in ONE packed pass (GEMM M = sum of prompt lengths, rounded to 256 rows);
-        attention per sequence through cram_attn_prefill_varlen; K/V scattered into the cache."""
+    def prefill(self, max_rows: int = PREFILL_CHUNK_ROWS):
+        """All prompts in packed varlen passes of at most ``max_rows`` tokens each (GEMM M = the chunk's token
+        count rounded to 256 rows; attention per sequence through cram_attn_prefill_varlen; K/V scattered into
+        the cache).  Chunks of the sweep's GEMM size run the GEMMs at the same rate as one huge pass, keep the
+        activations ~8x smaller and — every chunk having the same shape bound — let the caching allocator reuse
+        the same blocks across chunks and calls (one 231k-row pass made it map fresh multi-GB segments, a ~1 s
+        host stall per call)."""
+        b0 = 0
+        while b0 < self.B:
+            b1, rows = b0, 0
+            while b1 < self.B and (b1 == b0 or rows + self.lens[b1] <= max_rows):
+                rows += self.lens[b1]
+                b1 += 1
+            self._prefill_chunk(b0, b1)
+            b0 = b1
+        self.out[:, 0] = self.tokens
+        self.t.fill_(1)
+
+    def _prefill_chunk(self, b0: int, b1: int):
         eng, sp = self.eng, self.eng.spec
         dev = eng.device
-        lens = self.lens
+        lens = self.lens[b0:b1]
         total = sum(lens)
         Mp = padded_rows(total)
         offs = [0]
         for n in lens:
             offs.append(offs[-1] + n)
-        cu = torch.tensor(offs, dtype=torch.int32, device=dev)
-        pos = torch.cat([torch.arange(n, device=dev) for n in lens])
-        bidx = torch.cat([torch.full((n,), b, device=dev, dtype=torch.long) for b, n in enumerate(lens)])
+        cu = torch.tensor(offs, dtype=torch.int32).to(dev, non_blocking=True)
+        pos = torch.cat([torch.arange(n, dtype=torch.long) for n in lens]).to(dev, non_blocking=True)
+        bidx = torch.cat([torch.full((n,), b, dtype=torch.long) for b, n in enumerate(lens, b0)]).to(
+            dev, non_blocking=True)
         h = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=dev)
-        h[:total] = eng.embed[torch.cat(self.prompts)]
+        h[:total] = eng.embed[torch.cat(self.prompts[b0:b1])]
         if Mp > total:
             h[total:].zero_()
+        bias = self.cb.bias[b0:b1]
         m = None                                     # pending MLP output: layer output = h + m (add fused below)
         for l, lw in enumerate(eng.layers):
             if m is None:
@@ -400,16 +420,14 @@ class DecodeSession:
             a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
             if Mp > total:
                 a[total:].zero_()
-            ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=self.cb.bias,
-                                    enable=self.cb.enable[l], W=self.cb.W,
+            ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=bias,
+                                    enable=self.cb.enable[l, b0:b1], W=self.cb.W,
                                     out=a[:total].view(total, sp.num_heads, sp.head_dim))
             h, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
             m = eng.mlp(x2, lw)
         last = cu[1:].long() - 1
         _, hn = ops.rmsnorm(m[last], eng.norm, sp.eps, residual=h[last])
-        self.tokens.copy_(self._pick(ops.linear(hn, eng.lm_head)))
-        self.out[:, 0] = self.tokens
-        self.t.fill_(1)
+        self.tokens[b0:b1] = self._pick(ops.linear(hn, eng.lm_head))
 
     def _step_body(self):
         eng = self.eng

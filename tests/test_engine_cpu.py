@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from cram_amd import spans as S
-from cram_amd.engine import CrAMEngine
+from cram_amd.engine import CrAMEngine, DecodeSession
 from cram_amd import sweep
 from oracle import hook_ref
 from tests import cpu_ops
@@ -201,7 +201,13 @@ def test_engine_batched_generate_matches_single(tiny, nq):
     with cpu_ops.patched_ops():
         both = eng.generate(prompts, ws, heads, max_new_tokens=5, use_graph=False)
         one = [eng.generate([p], [w], heads, max_new_tokens=5, use_graph=False)[0] for p, w in zip(prompts, ws)]
+        # chunked packed prefill (chunks of <= 340 tokens: [200], [137, 171]) == one pass
+        chunked, whole = DecodeSession(eng, prompts, ws, heads, 5), DecodeSession(eng, prompts, ws, heads, 5)
+        chunked.prefill(max_rows=340)
+        whole.prefill()
     assert both == one
+    assert chunked.tokens.tolist() == whole.tokens.tolist() == [r[0] for r in both]
+    assert torch.equal(chunked.k_cache, whole.k_cache) and torch.equal(chunked.v_cache, whole.v_cache)
     # and against the hooked transformers model
     hs = hook_ref.register_hooks(model, heads, hook_ref.log_weight(ws[1]))
     try:
