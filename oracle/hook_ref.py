@@ -81,16 +81,17 @@ def edit_attention_mask(num_heads: int, hidden_states: torch.Tensor, attention_m
         T = hidden_states.shape[1]
         S = int(position_ids[0][-1]) + 1
         if T == 1:
-            mask = torch.zeros((1, 1, 1, S), dtype=dt)
+            mask = torch.zeros((1, 1, 1, S), dtype=dt, device=hidden_states.device)
         else:
-            mask = torch.triu(torch.full((T, S), torch.finfo(dt).min, dtype=dt), diagonal=1)[None, None]
+            mask = torch.triu(torch.full((T, S), torch.finfo(dt).min, dtype=dt, device=hidden_states.device),
+                              diagonal=1)[None, None]
     else:
         mask = attention_mask.clone()
     if mask.shape[1] == 1:
         mask = mask.repeat(1, num_heads, 1, 1)
     mask = mask.clone()
     B, H, T, S = mask.shape
-    row = lw.reshape(-1).to(dt)
+    row = lw.reshape(-1).to(device=mask.device, dtype=dt)
     rows = row.expand(T, W)
     for h in head_idx:
         sub = mask[:, h, :, :W]
