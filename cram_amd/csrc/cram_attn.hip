@@ -16,6 +16,9 @@
 //                            K/V tiles land in double-buffered LDS by LDS-DMA
 //                            (buffer_load ... lds, issued one tile ahead, one barrier
 //                            per tile); a workgroup = the query heads of one kv head.
+//                            V^T reads are inline asm (through the builtin the waitcnt
+//                            pass drains the K/V prefetch with vmcnt(0) before PV);
+//                            O leaves through LDS as whole-row 16-byte stores.
 //   decode_kernel<D,G>       q_len == 1, HBM-bound: 16 lanes per key row (16 B each,
 //                            DPP row reductions), all G query heads of a kv head per
 //                            workgroup, optional split over keys + combine_kernel.
@@ -82,6 +85,79 @@ __device__ __forceinline__ float half_sum(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// V^T fragment reads by inline asm: through the builtin, the waitcnt pass treats every ds_read_b64_tr_b16 as
+// aliasing the pending LDS-DMA and puts vmcnt(0) in front of it, which would drain the K/V prefetch every tile
+// (the .s of prefill_kernel shows it before its PV).  The reads of one 32-key block: 16 x 8 bytes, ordered
+// (half, db, s2) -> rr[s2 * 8 + db * 2 + half]; the caller waits on lgkmcnt before consuming them.
+template <int VSTR, int KB>
+__device__ __forceinline__ void tr_reads32(uint32_t a, i16x4 (&rr)[16]) {
+#define CRAM_TR(i, s2, db, h)                                                                     \
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2"                                              \
+               : "=v"(rr[i]) : "v"(a), "i"((KB * 32 + 16 * (s2) + 8 * (h)) * VSTR + (db) * 64))
+  CRAM_TR(0, 0, 0, 0); CRAM_TR(1, 0, 0, 1); CRAM_TR(2, 0, 1, 0); CRAM_TR(3, 0, 1, 1);
+  CRAM_TR(4, 0, 2, 0); CRAM_TR(5, 0, 2, 1); CRAM_TR(6, 0, 3, 0); CRAM_TR(7, 0, 3, 1);
+  CRAM_TR(8, 1, 0, 0); CRAM_TR(9, 1, 0, 1); CRAM_TR(10, 1, 1, 0); CRAM_TR(11, 1, 1, 1);
+  CRAM_TR(12, 1, 2, 0); CRAM_TR(13, 1, 2, 1); CRAM_TR(14, 1, 3, 0); CRAM_TR(15, 1, 3, 1);
+#undef CRAM_TR
+}
+
+// O^T[dv][q] += V^T[dv][key] . P^T[key][q] for the 32-key block KB of a tile (d = 128; V image of the tile at LDS
+// byte address vaddr - this lane's tr-read base): 16 V^T reads issued together, the first 8 MFMAs after lgkmcnt(8)
+// (LDS returns in order), the rest after lgkmcnt(0); sched_barrier keeps the MFMAs behind their waits
+template <typename T, int VSTR, int KB>
+__device__ __forceinline__ void pv_block32(uint32_t vaddr, const f32x16& pk, f32x16 (&oacc)[4]) {
+  using V8 = typename Vec<T>::x8;
+  V8 pb[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pb[s2][j] = (T)pk[8 * s2 + j];
+  i16x4 rr[16];
+  tr_reads32<VSTR, KB>(vaddr, rr);
+  asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int db = 0; db < 4; ++db)   // whole-vector bit casts (per-element extraction of tr results miscompiles)
+    oacc[db] = mfma32x16(__builtin_bit_cast(V8, __builtin_shufflevector(rr[2 * db], rr[2 * db + 1], 0, 1, 2, 3, 4, 5,
+                                                                        6, 7)), pb[0], oacc[db]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+    oacc[db] = mfma32x16(__builtin_bit_cast(V8, __builtin_shufflevector(rr[8 + 2 * db], rr[9 + 2 * db], 0, 1, 2, 3,
+                                                                        4, 5, 6, 7)), pb[1], oacc[db]);
+}
+
+// Epilogue of the prefill kernels: the wave's 32 output rows (lane (r, hh) holds row r's columns
+// db*32 + 8g + 4hh .. +3) are staged through LDS as model-dtype rows (stride 2D + 16 B) and stored as 16-byte
+// pieces of whole rows, 4 rows of d = 128 per instruction, instead of 16 scattered 8-byte stores per lane (the
+// store tail is issue-bound: MI355X_MICROARCH.md, attention epilogue).  Staging row i is output row
+// first_row + i * row_step; rows >= Tq are not stored.
+template <typename T, int D>
+__device__ __forceinline__ void store_o_rows(char* stage, const f32x16 (&oacc)[D / 32], float inv, int r, int hh,
+                                             int lane, T* obase, int64_t o_st, int first_row, int row_step, int Tq) {
+  using V4 = typename Vec<T>::x4;
+  using V8 = typename Vec<T>::x8;
+  constexpr int OSTR = D * 2 + 16;
+  constexpr int PPR = D * 2 / 16;              // 16-byte pieces per row
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      V4 o4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o4[e] = (T)(oacc[db][4 * g + e] * inv);
+      *reinterpret_cast<V4*>(stage + r * OSTR + (db * 32 + 8 * g + 4 * hh) * 2) = o4;
+    }
+#pragma unroll
+  for (int i = 0; i < 32 * PPR / 64; ++i) {
+    const int c = i * 64 + lane, row = c / PPR, pc = c % PPR;
+    const int qr = first_row + row * row_step;
+    const V8 v = *reinterpret_cast<const V8*>(stage + row * OSTR + pc * 16);
+    if (qr < Tq) *reinterpret_cast<V8*>(obase + (int64_t)qr * o_st + pc * 8) = v;
+  }
+}
+
 // Diagnostic build only (tools/stamp_prefill.hip defines CRAM_STAMPS): every wave takes s_memtime at the
 // phase boundaries of each tile into registers, accumulates the per-phase deltas and lane 0 writes the
 // sums once at the end (no stores inside the loop: CDNA4's vmcnt counts stores, so per-tile stamp stores
@@ -131,7 +207,6 @@ template <typename T, int D, int BK = 64, int OCC = 2>
 __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   using C = PrefillCfg<D, BK>;
   using V8 = typename Vec<T>::x8;
-  using V4 = typename Vec<T>::x4;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
 
   // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each XCD a
@@ -284,15 +359,8 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
       const char* base = smem + (t & 1) * C::STAGE;
       f32x16 sacc[C::NKB];
       const f32x16 zero16 = {};
-      // diagonal tile whose upper 32-key block lies past every query row of this wave (causal): that block's
-      // QK^T, softmax and PV are skipped (wave-uniform; its probabilities would all be exactly 0)
-      const bool hi_dead = C::NKB == 2 && key0 + 32 > wave_qpos_max;
 #pragma unroll
       for (int kb = 0; kb < C::NKB; ++kb) {
-        if (kb == 1 && hi_dead) {
-          sacc[kb] = zero16;
-          continue;
-        }
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
           const V8 a = *reinterpret_cast<const V8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
@@ -329,7 +397,6 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
         const int lim = min(qpos, S - 1) - key0;
 #pragma unroll
         for (int kb = 0; kb < C::NKB; ++kb) {
-          if (kb == 1 && hi_dead) continue;
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             f32x4 bv = {0.f, 0.f, 0.f, 0.f};
@@ -368,7 +435,6 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
         const float sc = plain ? p.scale_log2 : 1.f;
 #pragma unroll
         for (int kb = 0; kb < C::NKB; ++kb) {
-          if (kb == 1 && hi_dead) continue;
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const float pe = fast_exp2(__builtin_fmaf(sacc[kb][e], sc, -muse));
@@ -392,9 +458,13 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
 
       // O^T[dv][q] += V^T[dv][key] . P^T[key][q]
       const char* vimg = base + C::V_OFF;
+      if constexpr (D == 128) {     // V^T reads by inline asm (tr_reads32): the K/V prefetch stays in flight
+        const uint32_t vaddr = (uint32_t)(uintptr_t)(const lds_void*)vimg + (uint32_t)(tr_key * C::VSTR + tr_col * 2);
+        pv_block32<T, C::VSTR, 0>(vaddr, sacc[0], oacc);
+        if constexpr (C::NKB == 2) pv_block32<T, C::VSTR, 1>(vaddr, sacc[1], oacc);
+      } else
 #pragma unroll
       for (int kb = 0; kb < C::NKB; ++kb) {
-        if (kb == 1 && hi_dead) continue;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           V8 pb;
@@ -436,19 +506,9 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   if (lane == 0)
     for (int k = 0; k < 7; ++k) g_stamps[((size_t)wid * 4 + wave) * 8 + k] = acc_[k];
 #endif
-  if (qrow < Tq) {
-    const float inv = l > 0.f ? 1.f / l : 0.f;
-    T* ob = static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh + qrow * p.o_st;
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        V4 o4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o4[e] = (T)(oacc[db][4 * g + e] * inv);
-        *reinterpret_cast<V4*>(ob + db * 32 + 8 * g + 4 * hh) = o4;
-      }
-  }
+  // every wave passed the last tile's barrier: the stages are free for the O staging rows
+  store_o_rows<T, D>(smem + wave * 32 * (D * 2 + 16), oacc, l > 0.f ? 1.f / l : 0.f, r, hh, lane,
+                     static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh, p.o_st, q_row0, 1, Tq);
 }
 
 // --------------------------------------------------------------------------------------------

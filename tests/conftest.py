@@ -21,3 +21,14 @@ def gpu_device():
     from cram_amd import build
     build.build()
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=["bk64", "bk32"])
+def prefill_variant(request, monkeypatch):
+    """Run a prefill test on both d=128 prefill kernels: the default 64-key tiles at two waves per SIMD and the
+    opt-in 32-key tiles at three (CRAM_PREFILL_VARIANT=3).  The library reads the variable at every launch."""
+    if request.param == "bk32":
+        monkeypatch.setenv("CRAM_PREFILL_VARIANT", "3")
+    else:
+        monkeypatch.delenv("CRAM_PREFILL_VARIANT", raising=False)
+    return request.param

@@ -48,7 +48,7 @@ def _bias16(B, Hq, W, gen):
 @pytest.mark.parametrize("B,Hq,Hkv,T,d", [(1, 40, 40, 300, 128), (2, 8, 2, 200, 128), (1, 4, 4, 129, 64),
                                           (1, 4, 1, 1, 128)])
 @pytest.mark.parametrize("biased", [False, True])
-def test_prefill_fp16(gpu_device, B, Hq, Hkv, T, d, biased):
+def test_prefill_fp16(gpu_device, prefill_variant, B, Hq, Hkv, T, d, biased):
     from cram_amd import ops
     gen = torch.Generator().manual_seed(17 * T + Hq + biased)
     q = torch.randn(B, T, Hq, d, generator=gen).to(F16).transpose(1, 2)
@@ -66,7 +66,7 @@ def test_prefill_fp16(gpu_device, B, Hq, Hkv, T, d, biased):
     _check(out, ref)
 
 
-def test_prefill_fp16_zero_bias_is_no_bias(gpu_device):
+def test_prefill_fp16_zero_bias_is_no_bias(gpu_device, prefill_variant):
     """fp16 instantiation keeps the bf16 kernel's property: a zero bias is bit-identical to no bias."""
     from cram_amd import ops
     dev = gpu_device
@@ -104,7 +104,7 @@ def test_decode_fp16(gpu_device, B, Hq, Hkv, S, splits):
     _check(out, ref)
 
 
-def test_varlen_fp16(gpu_device):
+def test_varlen_fp16(gpu_device, prefill_variant):
     from cram_amd import ops
     lens, Hq, Hkv, d = [17, 300, 1, 129], 8, 8, 128
     gen = torch.Generator().manual_seed(99)

@@ -45,7 +45,7 @@ def _check(out, ref):
     (1, 8, 2, 900, 128), (1, 7, 1, 257, 128), (2, 4, 1, 200, 64), (1, 32, 8, 130, 128),
 ])
 @pytest.mark.parametrize("biased", [False, True])
-def test_prefill_matches_oracle(gpu_device, B, Hq, Hkv, T, d, biased):
+def test_prefill_matches_oracle(gpu_device, prefill_variant, B, Hq, Hkv, T, d, biased):
     gen = torch.Generator().manual_seed(1000 * T + 10 * Hq + d + biased)
     S = T
     # q laid out like transformers' transposed view: physical [B, T, Hq, d]
@@ -68,7 +68,7 @@ def test_prefill_matches_oracle(gpu_device, B, Hq, Hkv, T, d, biased):
     _check(out, ref)
 
 
-def test_prefill_query_offset(gpu_device):
+def test_prefill_query_offset(gpu_device, prefill_variant):
     """q_len < S (queries start at q_pos0 = S - Tq), as in chunked prefill / cached suffix."""
     gen = torch.Generator().manual_seed(7)
     B, Hq, Hkv, S, T, d = 1, 8, 2, 333, 45, 128
@@ -214,7 +214,7 @@ def test_silu_mul_matches_transformers(gpu_device, F):
 
 
 @pytest.mark.parametrize("lens,Hq,Hkv", [([17, 300, 1, 129], 8, 2), ([900, 77], 32, 8), ([5, 6, 7], 7, 1)])
-def test_prefill_varlen_matches_oracle(gpu_device, lens, Hq, Hkv):
+def test_prefill_varlen_matches_oracle(gpu_device, prefill_variant, lens, Hq, Hkv):
     """Packed sequences (cu_seqlens) in one launch == each sequence through the oracle."""
     from cram_amd import ops
     gen = torch.Generator().manual_seed(sum(lens))
@@ -264,7 +264,7 @@ def _rows_ref(q, k, v, bias, enable, W, scale, b, h, rows, G):
 
 
 @pytest.mark.parametrize("B,T", [(33, 962), (1, 8300)])
-def test_prefill_full_size_properties(gpu_device, B, T):
+def test_prefill_full_size_properties(gpu_device, prefill_variant, B, T):
     """BASELINE sizes (the IE sweep's 33-variant batch at T' = 962; config 5's 8k prompt), Llama-3 GQA 32/8.
     Size-independent properties, bit-exact: zero bias on every head == no bias; each batch element equals
     its own single-sequence launch; two q-heads of one GQA group with equal queries give equal outputs.
@@ -306,7 +306,7 @@ def test_prefill_full_size_properties(gpu_device, B, T):
             _check(oc[b, rows, h], ref)
 
 
-def test_varlen_full_size_equals_dense(gpu_device):
+def test_varlen_full_size_equals_dense(gpu_device, prefill_variant):
     """Config 2's packed prefill shape (64 prompts of 700-1100 tokens): every packed sequence equals its own
     dense single-sequence launch bit for bit (same tiles, same arithmetic)."""
     from cram_amd import ops

@@ -1,0 +1,44 @@
+"""Same-process interleaved A/B of prefill-kernel variants (CRAM_PREFILL_VARIANT is read by the library at every
+launch): N rounds x variants x shapes, median ms per launch.  Usage: python tools/ab_prefill_inproc.py f0 f7 ..."""
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cram_amd import ops  # noqa: E402
+
+variants = sys.argv[1:] or ["0", "f7"]
+dev = torch.device("cuda:0")
+d = 128
+shapes = [(33, 962), (1, 8300)]
+data = {}
+for B, T in shapes:
+    y = torch.randn(B, T, (32 + 16) * d, device=dev).to(torch.bfloat16)
+    q = y[..., :32 * d].unflatten(-1, (32, d)).transpose(1, 2)
+    k = y[..., 32 * d:40 * d].unflatten(-1, (8, d)).transpose(1, 2)
+    v = y[..., 40 * d:].unflatten(-1, (8, d)).transpose(1, 2)
+    data[(B, T)] = (q, k, v, torch.empty(B, T, 32, d, device=dev, dtype=torch.bfloat16))
+res = {(vv, s): [] for vv in variants for s in shapes}
+for rnd in range(5):
+    for vv in variants:
+        os.environ["CRAM_PREFILL_VARIANT"] = vv
+        for s in shapes:
+            q, k, v, out = data[s]
+            for _ in range(2):
+                ops.attn_prefill(q, k, v, scale=d ** -0.5, out=out)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                ops.attn_prefill(q, k, v, scale=d ** -0.5, out=out)
+            e1.record()
+            torch.cuda.synchronize()
+            res[(vv, s)].append(e0.elapsed_time(e1) / 10)
+for vv in variants:
+    line = []
+    for B, T in shapes:
+        ms = statistics.median(res[(vv, (B, T))])
+        fl, _ = ops.prefill_work(B, 32, 8, T, T, d, 0)
+        line.append(f"B={B} T={T}: {ms:.3f} ms {fl / ms / 1e9:.0f} TF")
+    print(f"variant {vv:>3}: " + " | ".join(line), flush=True)

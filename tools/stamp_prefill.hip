@@ -42,7 +42,7 @@ int main(int argc, char** argv) {
   unsigned long long* st;
   hipMalloc(&st, ns * 8);
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &st, sizeof(st));
-  for (int it = 0; it < 3; ++it) hipLaunchKernelGGL((prefill_kernel<128, 64, 2>), dim3(p.nblocks), dim3(256), 0, 0, p);
+  for (int it = 0; it < 3; ++it) hipLaunchKernelGGL((prefill_kernel<__bf16, 128, 64, 2>), dim3(p.nblocks), dim3(256), 0, 0, p);
   hipDeviceSynchronize();
   std::vector<unsigned long long> h(ns);
   hipMemcpy(h.data(), st, ns * 8, hipMemcpyDeviceToHost);
