@@ -129,7 +129,7 @@ __device__ __forceinline__ void pv_block32(uint32_t vaddr, const f32x16& pk, f32
 }
 
 // Epilogue of the prefill kernels: the wave's 32 output rows (lane (r, hh) holds row r's columns
-// db*32 + 8g + 4hh .. +3) are staged through LDS as model-dtype rows (stride 2D + 16 B) and stored as 16-byte
+// db*32 + 8g + 4hh .. +3) are staged through LDS as model-dtype rows (2D bytes each) and stored as 16-byte
 // pieces of whole rows, 4 rows of d = 128 per instruction, instead of 16 scattered 8-byte stores per lane (the
 // store tail is issue-bound: MI355X_MICROARCH.md, attention epilogue).  Staging row i is output row
 // first_row + i * row_step; rows >= Tq are not stored.
@@ -138,7 +138,7 @@ __device__ __forceinline__ void store_o_rows(char* stage, const f32x16 (&oacc)[D
                                              int lane, T* obase, int64_t o_st, int first_row, int row_step, int Tq) {
   using V4 = typename Vec<T>::x4;
   using V8 = typename Vec<T>::x8;
-  constexpr int OSTR = D * 2 + 16;
+  constexpr int OSTR = D * 2;                  // unpadded rows; the 16-byte pieces are XOR-swizzled by row
   constexpr int PPR = D * 2 / 16;              // 16-byte pieces per row
 #pragma unroll
   for (int db = 0; db < D / 32; ++db)
@@ -147,13 +147,15 @@ __device__ __forceinline__ void store_o_rows(char* stage, const f32x16 (&oacc)[D
       V4 o4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o4[e] = (T)(oacc[db][4 * g + e] * inv);
-      *reinterpret_cast<V4*>(stage + r * OSTR + (db * 32 + 8 * g + 4 * hh) * 2) = o4;
+      // piece db*4 + g of row r lands at piece (db*4 + g) ^ (r mod PPR): the 16 rows of a ds_write_b64 lane group
+      // spread over the banks (2-way), and the row-contiguous read-back below is conflict-free
+      *reinterpret_cast<V4*>(stage + r * OSTR + ((db * 4 + g) ^ (r & (PPR - 1))) * 16 + hh * 8) = o4;
     }
 #pragma unroll
   for (int i = 0; i < 32 * PPR / 64; ++i) {
     const int c = i * 64 + lane, row = c / PPR, pc = c % PPR;
     const int qr = first_row + row * row_step;
-    const V8 v = *reinterpret_cast<const V8*>(stage + row * OSTR + pc * 16);
+    const V8 v = *reinterpret_cast<const V8*>(stage + row * OSTR + (pc ^ (row & (PPR - 1))) * 16);
     if (qr < Tq) *reinterpret_cast<V8*>(obase + (int64_t)qr * o_st + pc * 8) = v;
   }
 }
@@ -507,7 +509,7 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
     for (int k = 0; k < 7; ++k) g_stamps[((size_t)wid * 4 + wave) * 8 + k] = acc_[k];
 #endif
   // every wave passed the last tile's barrier: the stages are free for the O staging rows
-  store_o_rows<T, D>(smem + wave * 32 * (D * 2 + 16), oacc, l > 0.f ? 1.f / l : 0.f, r, hh, lane,
+  store_o_rows<T, D>(smem + wave * 32 * (D * 2), oacc, l > 0.f ? 1.f / l : 0.f, r, hh, lane,
                      static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh, p.o_st, q_row0, 1, Tq);
 }
 
