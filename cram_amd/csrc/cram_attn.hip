@@ -205,10 +205,11 @@ struct PrefillCfg {
   static constexpr int LDS = 2 * STAGE;
 };
 
-template <typename T, int D, int BK = 64, int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
+template <typename T, int D, int BK = 64, int OCC = 2, int NW = 4>
+__global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) {
   using C = PrefillCfg<D, BK>;
   using V8 = typename Vec<T>::x8;
+  static_assert(C::LDS >= NW * 32 * D * 2, "O staging rows must fit in the K/V stages");
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
 
   // XCD-aware bijective remap: blocks b and b+8 share an XCD, so give each XCD a
@@ -216,9 +217,9 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  // a workgroup = hp query heads of ONE kv head (GQA group) x (4 / hp) waves of 32 query rows:
+  // a workgroup = hp query heads of ONE kv head (GQA group) x (NW / hp) waves of 32 query rows:
   // every K/V tile staged in LDS feeds hp heads, and waves that share rows finish together
-  const int hp = p.hp, rw = 4 / hp, BQ = 32 * rw;
+  const int hp = p.hp, rw = NW / hp, BQ = 32 * rw;
   const int nhg = p.Hq / hp;
   const int qi_blk = wid % p.nqb;
   const int bh = wid / p.nqb;
@@ -283,11 +284,11 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
   // the 16 bytes that belong at image offset c*1024 + 16p (a pad slot gets an out-of-range offset, so
   // the descriptor's range check writes zeros there, as it does for rows past key S).
   constexpr int KCH = C::KCH, NCH = C::KCH + C::VCH;
-  constexpr int CPW = (NCH + 3) / 4;           // chunks per wave per tile
+  constexpr int CPW = (NCH + NW - 1) / NW;     // chunks per wave per tile
   uint32_t doff[CPW];
 #pragma unroll
   for (int i = 0; i < CPW; ++i) {
-    const int c = wave + 4 * i;
+    const int c = wave + NW * i;
     uint32_t off = 0xFFFFFFF0u;
     if (c < KCH) {
       const int x = c * 1024 + 16 * lane, row = x / C::KSTR, colb = x % C::KSTR;
@@ -310,7 +311,7 @@ __global__ __launch_bounds__(256, OCC) void prefill_kernel(PrefillParams p) {
     char* base = smem + (t & 1) * C::STAGE;
 #pragma unroll
     for (int i = 0; i < CPW; ++i) {
-      const int c = wave + 4 * i;
+      const int c = wave + NW * i;
       if (c < KCH)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (lds_void*)(base + c * 1024), 16, (int)doff[i], 0, 0, 0);
       else if (c < NCH)
@@ -743,17 +744,22 @@ template <typename T, int D>
 int launch_prefill(PrefillParams& p, hipStream_t stream) {
   const int G = p.Hq / p.Hkv;
   p.hp = (G % 4 == 0) ? 4 : (G % 2 == 0) ? 2 : 1;
-  const int bq = 32 * (4 / p.hp);
+  // CRAM_PREFILL_VARIANT=3 (opt-in): 32-key tiles, 162 VGPRs -> three waves per SIMD; +4 % at the sweep
+  // shape, but on the tiny Qwen2 model its IE noise doubled on one question and broke the parity bar
+  // (tools/ie_noise_probe.py), so 64-key tiles at two waves per SIMD stay the default.
+  // CRAM_PREFILL_VARIANT=8: 8-wave workgroups (one per CU), every K/V tile feeds twice the query rows.
+  const char* e = getenv("CRAM_PREFILL_VARIANT");
+  const int var = (D == 128 && e && (e[0] == '3' || e[0] == '8')) ? e[0] - '0' : 0;
+  const int nw = var == 8 ? 8 : 4;
+  const int bq = 32 * (nw / p.hp);
   p.nqb = (p.Tq + bq - 1) / bq;
   const int64_t nblocks = (int64_t)p.nqb * (p.Hq / p.hp) * p.B;
   if (nblocks > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
   p.nblocks = (int)nblocks;
-  // CRAM_PREFILL_VARIANT=3 (opt-in): 32-key tiles, 162 VGPRs -> three waves per SIMD; +4 % at the sweep
-  // shape, but on the tiny Qwen2 model its IE noise doubled on one question and broke the parity bar
-  // (tools/ie_noise_probe.py), so 64-key tiles at two waves per SIMD stay the default
-  const char* e = getenv("CRAM_PREFILL_VARIANT");
-  if (D == 128 && e && e[0] == '3')
+  if (var == 3)
     hipLaunchKernelGGL((prefill_kernel<T, D, 32, 3>), dim3(p.nblocks), dim3(256), 0, stream, p);
+  else if (var == 8)
+    hipLaunchKernelGGL((prefill_kernel<T, D, 64, 1, 8>), dim3(p.nblocks), dim3(512), 0, stream, p);
   else
     hipLaunchKernelGGL((prefill_kernel<T, D, 64, 2>), dim3(p.nblocks), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;

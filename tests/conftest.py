@@ -23,12 +23,13 @@ def gpu_device():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=["bk64", "bk32"])
+@pytest.fixture(params=["bk64", "bk32", "w8"])
 def prefill_variant(request, monkeypatch):
-    """Run a prefill test on both d=128 prefill kernels: the default 64-key tiles at two waves per SIMD and the
-    opt-in 32-key tiles at three (CRAM_PREFILL_VARIANT=3).  The library reads the variable at every launch."""
-    if request.param == "bk32":
-        monkeypatch.setenv("CRAM_PREFILL_VARIANT", "3")
+    """Run a prefill test on every d=128 prefill kernel: the default 64-key tiles at two waves per SIMD, the
+    opt-in 32-key tiles at three (CRAM_PREFILL_VARIANT=3) and the 8-wave workgroups (=8).  The library reads
+    the variable at every launch."""
+    if request.param in ("bk32", "w8"):
+        monkeypatch.setenv("CRAM_PREFILL_VARIANT", {"bk32": "3", "w8": "8"}[request.param])
     else:
         monkeypatch.delenv("CRAM_PREFILL_VARIANT", raising=False)
     return request.param
