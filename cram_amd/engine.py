@@ -24,7 +24,7 @@ from typing import List, Optional, Sequence
 
 import torch
 
-from . import ops
+from . import gemm_tune, ops
 from .bias import CredibilityBias
 
 
@@ -89,8 +89,9 @@ def padded_rows(M: int) -> int:
 
 
 def configure_blas(lib: str = "hipblas") -> None:
-    """Select torch's GEMM backend.  On MI355X rocBLAS ("hipblas") beat hipBLASLt by 2.7% per
-    Llama-3-8B layer at M = 31744 (QKV N = 6144: 1.09 vs 1.30 ms; tools/gemm_bench.py)."""
+    """Select torch's default GEMM backend.  hipBLASLt and rocBLAS measure equal per Llama-3-8B layer at the sweep's
+    row counts (tools/gemm_bench.py; an earlier 13 % QKV gap was a cold-clock ordering artefact) and in the full
+    bench; the shapes where the default pick is slow are pinned by gemm_tune."""
     torch.backends.cuda.preferred_blas_library(lib)
 
 
@@ -111,6 +112,8 @@ class CrAMEngine:
         self.device = embed.device
         self.dtype = embed.dtype
         self.scale = spec.head_dim ** -0.5
+        if self.device.type == "cuda":
+            gemm_tune.ensure()          # pinned q/k/v and o_proj GEMM solutions (no-op on another BLAS build)
 
     # ------------------------------------------------------------------ construction
     SUPPORTED = ("llama", "qwen2")

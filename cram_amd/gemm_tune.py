@@ -1,0 +1,84 @@
+"""Pinned GEMM solutions for the IE sweep's projection shapes, through PyTorch TunableOp's results file.
+
+hipBLASLt's heuristic pick for the sweep's q/k/v (N = 6144) and o_proj (N = 4096, K = 4096) GEMMs at
+M = 33 x T rows is 9-12 % slower than the best solution TunableOp finds (`tools/tunable_probe.py`, same-process
+A/B: 8.86 -> 8.55 ms per Llama-3-8B layer at M = 29184).  Tuning online is not an option (every question has
+its own M = 33 x T rounded to 256), so the solutions tuned once are pinned for every M the sweep and the packed
+prefill can produce: a TunableOp results file is written at start-up with one line per (N, K, M) and read
+back with tuning off.  Shapes without a line (decode steps, other models) run the default heuristic.
+
+The solution ids belong to one hipBLASLt / rocBLAS build: the file carries the validators of the build they
+were tuned on (`data/gemm_solutions.json`), and nothing is pinned when the running build differs.
+"""
+from __future__ import annotations
+
+import json
+import os
+import tempfile
+from typing import Dict, Iterable, Tuple
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SOLUTIONS = os.path.join(REPO, "data", "gemm_solutions.json")
+_installed = None
+_tried = None
+
+
+def _signature(N: int, K: int, M: int) -> str:
+    # F.linear(x [M, K], w [N, K]) is a column-major TN GEMM with m = N, n = M, k = K
+    return f"tn_{N}_{M}_{K}_ld_{K}_{K}_{N}"
+
+
+def load(path: str = SOLUTIONS) -> dict:
+    with open(path) as f:
+        return json.load(f)
+
+
+def validators_match(tuned: Dict[str, str]) -> bool:
+    try:
+        have = {str(v[0]): str(v[1]) for v in torch.cuda.tunable.get_validators()}   # (name, value) pairs
+    except (RuntimeError, IndexError, TypeError):
+        return False
+    return all(have.get(k) == v for k, v in tuned.items())
+
+
+def install(m_values: Iterable[int], dtype: str = "BFloat16", path: str = SOLUTIONS) -> bool:
+    """Pin the tuned solutions for every M in m_values; returns False (nothing pinned) on a different build."""
+    global _installed
+    sol = load(path)
+    if not validators_match(sol["validators"]):
+        return False
+    lines = [f"Validator,{k},{v}" for k, v in sol["validators"].items()]
+    for key, name in sol["solutions"].items():
+        N, K = (int(x) for x in key.split("x"))
+        for M in m_values:
+            lines.append(f"GemmTunableOp_{dtype}_TN,{_signature(N, K, M)},{name},0")
+    fd, fn = tempfile.mkstemp(prefix="cram_gemm_", suffix=".csv")
+    with os.fdopen(fd, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    torch.cuda.tunable.enable(True)
+    torch.cuda.tunable.tuning_enable(False)
+    torch.cuda.tunable.record_untuned_enable(False)
+    ok = torch.cuda.tunable.read_file(fn)
+    os.unlink(fn)
+    _installed = fn if ok else None
+    return bool(ok)
+
+
+def sweep_rows(lo: int = 8192, hi: int = 65536, step: int = 256) -> Tuple[int, ...]:
+    """Row counts the sweep's suffix batches (33 x T, rounded up to 256) and the packed prefill chunks take."""
+    return tuple(range(lo, hi + 1, step))
+
+
+def ensure() -> bool:
+    """Install the pins once per process (CrAMEngine does this on a GPU); False when the build differs."""
+    global _tried
+    if _tried is None:
+        off = os.environ.get("CRAM_GEMM_PIN", "1") == "0"              # A/B switch: default heuristic everywhere
+        _tried = install(sweep_rows()) if torch.cuda.is_available() and not off else False
+    return _tried
+
+
+def uninstall() -> None:
+    torch.cuda.tunable.enable(False)

@@ -117,3 +117,15 @@ def test_metric_edge_cases():
     assert M.exact_match("The Answer!", ["answer"]) is True
     assert M.f1_score("", "") == 1
     assert M.f1_score("a b", "c") == 0
+
+
+def test_gemm_pin_file_signatures():
+    """The pinned GEMM lines use TunableOp's own signature for F.linear (x [M, K] @ w[N, K]^T = TN, m = N, n = M)
+    as written by a tuning run (tools/tunable_probe.py), and every pinned shape is a Llama-3-8B projection."""
+    from cram_amd import gemm_tune
+    assert gemm_tune._signature(6144, 4096, 29184) == "tn_6144_29184_4096_ld_4096_4096_6144"
+    sol = gemm_tune.load()
+    assert set(sol["solutions"]) <= {"6144x4096", "4096x4096", "28672x4096", "4096x14336"}
+    assert {"HIPBLASLT_VERSION", "ROCBLAS_VERSION", "GCN_ARCH_NAME"} <= set(sol["validators"])
+    rows = gemm_tune.sweep_rows()
+    assert rows[0] == 8192 and rows[-1] == 65536 and all(m % 256 == 0 for m in rows)
