@@ -105,7 +105,7 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     a_bias = eng.attention(q, k, v, bias, enable, W)                   # [1, rows, Hq, d] every head biased
     a_base = qc.a[l][:, -rows:]
     M = Hv * rows
-    Mp = M if last else padded_rows(M)                                  # GEMM rows aligned to the macro tile
+    Mp = M if last else padded_rows(M, sp)                              # GEMM rows: macro tile / measured table
     abuf = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=eng.device)
     x = abuf[:M].view(Hv, rows, H, sp.head_dim)
     x.copy_(a_base.expand(Hv, rows, H, sp.head_dim))                    # [Hv, rows, Hq, d]

@@ -264,3 +264,16 @@ def test_sweep_prefix_skip_is_exact(tiny, nq):
     T = ids.shape[1]
     assert sweep.sweep_flops(eng.spec, T, ans.numel(), p0) < sweep.sweep_flops(eng.spec, T, ans.numel())
 
+
+
+def test_padded_rows_table():
+    """GEMM row padding: a multiple of 256, never fewer rows, at most +2048 with the Llama-3-8B table; other
+    shapes (and no spec) keep plain 256-row rounding."""
+    from cram_amd.engine import ModelSpec, padded_rows
+    sp = ModelSpec.llama3_8b()
+    for M in list(range(1, 3000, 97)) + list(range(16000, 41000, 131)) + [70000]:
+        p = padded_rows(M, sp)
+        assert p % 256 == 0 and M <= p <= -(-M // 256) * 256 + 2048
+        assert padded_rows(M) == -(-M // 256) * 256
+        assert padded_rows(M, ModelSpec.qwen2_7b()) == padded_rows(M)
+    assert padded_rows(28050, sp) == 28672        # measured: 28672 rows (7 x 4096) run cheaper than 28160
