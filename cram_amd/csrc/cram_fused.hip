@@ -102,12 +102,16 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(const T* __restrict__ x, in
   }
 }
 
-// one thread = 8 rotation pairs (i, i + d/2) of one head of one row
-template <typename E>
+// one thread = 8 rotation pairs (i, i + d/2) of one head of one row.  SPLIT: the row's heads are q | k | v
+// (hq, then (heads - hq) / 2 each); q rotates in place, k rotates into kout and v is copied into vout, where
+// row r = b * T + t of the buffer lands at row kv_row0 + t of sequence b (batch stride kv_bs, row stride kv_rs):
+// the suffix K/V of the IE sweep go straight behind their shared prefix, with no separate copy pass
+template <typename E, bool SPLIT>
 __global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t rs, int rows, int T, int heads,
                                                    int d, const E* __restrict__ cos_t,
                                                    const E* __restrict__ sin_t, int64_t tab_rs,
-                                                   const int64_t* __restrict__ pos) {
+                                                   const int64_t* __restrict__ pos, int hq, E* __restrict__ kout,
+                                                   E* __restrict__ vout, int64_t kv_bs, int64_t kv_rs, int kv_row0) {
   using V8 = typename Vec<E>::x8;
   const unsigned half = (unsigned)d >> 1, vpp = half >> 3;  // vectors per half-row
   const unsigned gid = blockIdx.x * 256u + threadIdx.x;      // host guarantees rows*heads*vpp < 2^31
@@ -117,10 +121,23 @@ __global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t 
   const unsigned h = rh % (unsigned)heads;
   const unsigned row32 = rh / (unsigned)heads;
   const int64_t row = row32;
-  const int64_t p = pos ? pos[row] : (int64_t)(row32 % (unsigned)T);
   E* base = qkv + row * rs + (int64_t)h * d + vi * 8;
   const V8 x1 = *reinterpret_cast<const V8*>(base);
   const V8 x2 = *reinterpret_cast<const V8*>(base + half);
+  E* dst = base;
+  if (SPLIT && h >= (unsigned)hq) {
+    const unsigned hkv = ((unsigned)heads - (unsigned)hq) >> 1;
+    const bool is_v = h >= (unsigned)hq + hkv;
+    const unsigned hk = h - (unsigned)hq - (is_v ? hkv : 0u);
+    const int64_t b = row32 / (unsigned)T, t = row32 % (unsigned)T;
+    dst = (is_v ? vout : kout) + b * kv_bs + (kv_row0 + t) * kv_rs + (int64_t)hk * d + vi * 8;
+    if (is_v) {                                              // v: copied, not rotated
+      *reinterpret_cast<V8*>(dst) = x1;
+      *reinterpret_cast<V8*>(dst + half) = x2;
+      return;
+    }
+  }
+  const int64_t p = pos ? pos[row] : (int64_t)(row32 % (unsigned)T);
   const E* ct = cos_t + p * tab_rs + vi * 8;
   const E* st = sin_t + p * tab_rs + vi * 8;
   const V8 c1 = *reinterpret_cast<const V8*>(ct), c2 = *reinterpret_cast<const V8*>(ct + half);
@@ -133,8 +150,8 @@ __global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t 
     o1[j] = (E)(rnd<E>(a * (float)c1[j]) + rnd<E>(-b * (float)s1[j]));
     o2[j] = (E)(rnd<E>(b * (float)c2[j]) + rnd<E>(a * (float)s2[j]));
   }
-  *reinterpret_cast<V8*>(base) = o1;
-  *reinterpret_cast<V8*>(base + half) = o2;
+  *reinterpret_cast<V8*>(dst) = o1;
+  *reinterpret_cast<V8*>(dst + half) = o2;
 }
 
 template <typename T>
@@ -208,11 +225,39 @@ int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads,
   const dim3 g((unsigned)((total + 255) / 256));
   const hipStream_t st = (hipStream_t)stream;
   if (dtype == CRAM_DTYPE_BF16)
-    hipLaunchKernelGGL(rope_kernel<__bf16>, g, dim3(256), 0, st, (__bf16*)qkv, row_stride, rows, T, heads, d,
-                       (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos);
+    hipLaunchKernelGGL((rope_kernel<__bf16, false>), g, dim3(256), 0, st, (__bf16*)qkv, row_stride, rows, T, heads,
+                       d, (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos, heads, nullptr, nullptr, 0, 0, 0);
   else
-    hipLaunchKernelGGL(rope_kernel<_Float16>, g, dim3(256), 0, st, (_Float16*)qkv, row_stride, rows, T, heads, d,
-                       (const _Float16*)cos_t, (const _Float16*)sin_t, tab_rs, pos);
+    hipLaunchKernelGGL((rope_kernel<_Float16, false>), g, dim3(256), 0, st, (_Float16*)qkv, row_stride, rows, T,
+                       heads, d, (const _Float16*)cos_t, (const _Float16*)sin_t, tab_rs, pos, heads, nullptr, nullptr,
+                       0, 0, 0);
+  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}
+
+int cram_rope_split(void* qkv, int64_t row_stride, int rows, int T, int hq, int hkv, int d, const void* cos_t,
+                    const void* sin_t, int64_t tab_rs, const int64_t* pos, void* kout, void* vout, int64_t kv_bs,
+                    int64_t kv_rs, int kv_row0, int dtype, cram_stream_t stream) {
+  if (!qkv || !cos_t || !sin_t || !kout || !vout || rows < 0 || hq <= 0 || hkv <= 0 || T <= 0 || kv_row0 < 0 ||
+      rows % T != 0)
+    return CRAM_ERR_INVALID_ARG;
+  if (!dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
+  if (rows == 0) return CRAM_OK;
+  if ((d & 15) || !m8(row_stride) || !m8(tab_rs) || !m8(kv_bs) || !m8(kv_rs) || !al16(qkv) || !al16(cos_t) ||
+      !al16(sin_t) || !al16(kout) || !al16(vout))
+    return CRAM_ERR_ALIGNMENT;
+  const int heads = hq + 2 * hkv;
+  const int64_t total = (int64_t)rows * heads * (d / 16);
+  if (total >= (1ll << 31)) return CRAM_ERR_INVALID_ARG;
+  const dim3 g((unsigned)((total + 255) / 256));
+  const hipStream_t st = (hipStream_t)stream;
+  if (dtype == CRAM_DTYPE_BF16)
+    hipLaunchKernelGGL((rope_kernel<__bf16, true>), g, dim3(256), 0, st, (__bf16*)qkv, row_stride, rows, T, heads,
+                       d, (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos, hq, (__bf16*)kout, (__bf16*)vout,
+                       kv_bs, kv_rs, kv_row0);
+  else
+    hipLaunchKernelGGL((rope_kernel<_Float16, true>), g, dim3(256), 0, st, (_Float16*)qkv, row_stride, rows, T,
+                       heads, d, (const _Float16*)cos_t, (const _Float16*)sin_t, tab_rs, pos, hq, (_Float16*)kout,
+                       (_Float16*)vout, kv_bs, kv_rs, kv_row0);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 

@@ -279,22 +279,21 @@ class CrAMEngine:
             hbuf, x = ops.rmsnorm(delta, lw.ln1, sp.eps, residual=hbuf)
         y = ops.linear(x, lw.wqkv, lw.bqkv)
         yr = y[:M]
-        ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T,
-                         pos=None if prefix is None else prefix[2])
         y3 = yr.view(B, T, -1)
         q = y3[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
-        k = y3[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
-        v = y3[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
-        if prefix is not None:                       # [prefix | suffix] keys per sequence
-            k0, v0, _ = prefix
+        if prefix is None:
+            ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
+            k = y3[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
+            v = y3[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
+        else:                                        # [prefix | suffix] keys per sequence
+            k0, v0, pos = prefix
             p0 = k0.shape[1]
-            kf = torch.empty((B, p0 + T, sp.num_kv_heads, sp.head_dim), dtype=self.dtype, device=self.device)
-            vf = torch.empty_like(kf)
-            kf[:, :p0] = k0
-            kf[:, p0:] = k
-            vf[:, :p0] = v0
-            vf[:, p0:] = v
-            k, v = kf, vf
+            k = torch.empty((B, p0 + T, sp.num_kv_heads, sp.head_dim), dtype=self.dtype, device=self.device)
+            v = torch.empty_like(k)
+            k[:, :p0] = k0
+            v[:, :p0] = v0
+            # q roped in place; the suffix's roped k and its v land behind the prefix (no copy pass)
+            ops.rope_split(yr, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)
         if out_rows is None:
             a = torch.empty((hbuf.shape[0], sp.q_size), dtype=self.dtype, device=self.device)
             ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale, bias=bias,

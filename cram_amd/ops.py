@@ -295,6 +295,30 @@ def rope_inplace(qkv: torch.Tensor, heads: int, head_dim: int, cos: torch.Tensor
     return qkv
 
 
+def rope_split(qkv: torch.Tensor, hq: int, hkv: int, head_dim: int, cos: torch.Tensor, sin: torch.Tensor, T: int,
+               kout: torch.Tensor, vout: torch.Tensor, row0: int, pos: Optional[torch.Tensor] = None) -> None:
+    """RoPE over a fused q | k | v row buffer of B*T rows: q rotated in place, k rotated into kout[b, row0 + t] and v
+    copied into vout[b, row0 + t] (kout/vout [B, S, hkv, head_dim], rows contiguous)."""
+    y2 = _rows2d(qkv, "qkv")
+    dt = _dt(qkv)
+    rows = y2.shape[0]
+    if cos.dtype != qkv.dtype or sin.dtype != qkv.dtype or cos.shape != sin.shape or cos.stride(-1) != 1:
+        raise ValueError("cos/sin must be [P, d] tables of the QKV buffer's dtype")
+    if pos is not None and (pos.dtype != torch.int64 or pos.numel() != rows):
+        raise ValueError("pos must be int64 with one entry per row")
+    for t in (kout, vout):
+        if (t.dtype != qkv.dtype or t.device != qkv.device or t.dim() != 4 or t.shape[2:] != (hkv, head_dim)
+                or t.stride(3) != 1 or t.stride(2) != head_dim or t.shape[0] * T != rows or row0 + T > t.shape[1]):
+            raise ValueError("kout/vout must be [B, S >= row0 + T, hkv, head_dim] with contiguous rows, B * T rows")
+    if kout.stride()[:2] != vout.stride()[:2]:
+        raise ValueError("kout and vout must share their batch and row strides")
+    code = _lib.load().cram_rope_split(y2.data_ptr(), y2.stride(0), rows, int(T), int(hq), int(hkv), int(head_dim),
+                                       cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), kout.data_ptr(),
+                                       vout.data_ptr(), kout.stride(0), kout.stride(1), int(row0), dt,
+                                       _stream(qkv.device))
+    _lib.check(code, "cram_rope_split")
+
+
 def silu_mul(gu: torch.Tensor, F: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """rnd(silu(gu[..., :F])) * gu[..., F:2F] (LlamaMLP activation), bf16 or fp16."""
     _dt(gu)

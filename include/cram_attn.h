@@ -132,6 +132,10 @@ int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64
  * cram_rope_inplace  rotates the first `heads` heads (q then k) of every row of a fused QKV buffer in
  *                    place; row r uses position pos[r] (int64) or r % T when pos == NULL; cos/sin are
  *                    [P][d] tables of the same dtype (row stride tab_rs).
+ * cram_rope_split    the same rotation over a q | k | v row (hq, hkv, hkv heads): q in place, k rotated into
+ *                    kout and v copied into vout, buffer row r = b * T + t going to row kv_row0 + t of sequence
+ *                    b (batch stride kv_bs, row stride kv_rs, elements): the IE sweep's suffix K/V written
+ *                    behind their shared prefix (cram_amd/engine.py layer_rows) with no copy pass; rows % T == 0
  * cram_silu_mul      y[r, :F] = rnd(rnd(silu(gu[r, :F])) * gu[r, F:2F])
  */
 int cram_rmsnorm(const void* x, int64_t x_rs, const void* residual, int64_t r_rs, void* h_out, int64_t h_rs,
@@ -139,6 +143,9 @@ int cram_rmsnorm(const void* x, int64_t x_rs, const void* residual, int64_t r_rs
                  cram_stream_t stream);
 int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads, int d, const void* cos_t,
                       const void* sin_t, int64_t tab_rs, const int64_t* pos, int dtype, cram_stream_t stream);
+int cram_rope_split(void* qkv, int64_t row_stride, int rows, int T, int hq, int hkv, int d, const void* cos_t,
+                    const void* sin_t, int64_t tab_rs, const int64_t* pos, void* kout, void* vout, int64_t kv_bs,
+                    int64_t kv_rs, int kv_row0, int dtype, cram_stream_t stream);
 int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, int dtype,
                   cram_stream_t stream);
 

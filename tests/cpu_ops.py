@@ -101,6 +101,16 @@ def rope_inplace(qkv, heads, head_dim, cos, sin, T, pos=None):
     return qkv
 
 
+def rope_split(qkv, hq, hkv, head_dim, cos, sin, T, kout, vout, row0, pos=None):
+    y = qkv.reshape(-1, qkv.shape[-1])
+    rope_inplace(y, hq + hkv, head_dim, cos, sin, T, pos)
+    B = y.shape[0] // T
+    kv = hkv * head_dim
+    q_size = hq * head_dim
+    kout[:, row0:row0 + T] = y[:, q_size:q_size + kv].reshape(B, T, hkv, head_dim)
+    vout[:, row0:row0 + T] = y[:, q_size + kv:q_size + 2 * kv].reshape(B, T, hkv, head_dim)
+
+
 def silu_mul(gu, F, out=None):
     return torch.nn.functional.silu(gu[..., :F]) * gu[..., F:]
 
@@ -110,7 +120,7 @@ def patched_ops():
     """Route cram_amd.ops through the CPU stand-ins for the duration of a CPU test."""
     from cram_amd import ops
     names = ("attn_prefill", "attn_prefill_varlen", "attn_decode", "answer_logits", "decode_workspace_bytes",
-             "rmsnorm", "rope_inplace", "silu_mul")
+             "rmsnorm", "rope_inplace", "rope_split", "silu_mul")
     saved = {n: getattr(ops, n) for n in names}
     g = globals()
     for n in names:

@@ -17,7 +17,7 @@ def _declared():
 def test_header_declares_the_boundary():
     names = _declared()
     for n in ("cram_attn_prefill", "cram_attn_decode", "cram_attn_decode_workspace_size", "cram_answer_logits",
-              "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_silu_mul"):
+              "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_rope_split", "cram_silu_mul"):
         assert n in names
 
 

@@ -202,6 +202,38 @@ def test_rope_bit_exact(gpu_device, Hq, Hkv):
     assert torch.equal(y2[:, 0, :(Hq + Hkv) * d].unflatten(-1, (Hq + Hkv, d)), ref2)
 
 
+@pytest.mark.parametrize("Hq,Hkv,dtype", [(32, 8, torch.bfloat16), (28, 4, torch.bfloat16), (4, 2, torch.float16)])
+def test_rope_split_equals_inplace_plus_copy(gpu_device, Hq, Hkv, dtype):
+    """cram_rope_split (the IE sweep's suffix layers): q rotated in place and k/v written behind a prefix in
+    [B, p0 + T] buffers, bit-identical to cram_rope_inplace followed by the copies it replaces; per-row positions
+    p0 + t, a padded row buffer, and the prefix rows left untouched."""
+    from cram_amd import ops
+    from cram_amd.engine import CrAMEngine, ModelSpec
+    dev = gpu_device
+    d = 128
+    sp = ModelSpec(1, Hq * d, Hq, Hkv, d, 256, 100, 1e-5, False)
+    eng = CrAMEngine.random(sp, dev, seed=1, dtype=dtype)
+    B, T, p0 = 5, 77, 19
+    N = (Hq + 2 * Hkv) * d
+    cos, sin = eng.rope_tables(p0 + T)
+    ybuf = torch.randn(B * T + 64, N, device=dev).to(dtype)          # padded rows beyond B * T
+    pos = (torch.arange(T, device=dev) + p0).repeat(B)
+    y_ref = ybuf[:B * T].clone()
+    ops.rope_inplace(y_ref, Hq + Hkv, d, cos, sin, T, pos=pos)
+    y3 = y_ref.view(B, T, N)
+    k_ref = y3[..., Hq * d:(Hq + Hkv) * d].unflatten(-1, (Hkv, d))
+    v_ref = y3[..., (Hq + Hkv) * d:].unflatten(-1, (Hkv, d))
+    k = torch.randn(B, p0 + T, Hkv, d, device=dev).to(dtype)
+    v = torch.randn_like(k)
+    k_pre, v_pre = k[:, :p0].clone(), v[:, :p0].clone()
+    pad_before = ybuf[B * T:].clone()
+    ops.rope_split(ybuf[:B * T], Hq, Hkv, d, cos, sin, T, k, v, p0, pos=pos)
+    assert torch.equal(ybuf[:B * T, :Hq * d], y_ref[:, :Hq * d])
+    assert torch.equal(k[:, p0:], k_ref) and torch.equal(v[:, p0:], v_ref)
+    assert torch.equal(k[:, :p0], k_pre) and torch.equal(v[:, :p0], v_pre)
+    assert torch.equal(ybuf[B * T:], pad_before)
+
+
 @pytest.mark.parametrize("F", [512, 14336, 18944])
 def test_silu_mul_matches_transformers(gpu_device, F):
     from cram_amd import ops
