@@ -30,7 +30,49 @@ sys.path.insert(0, REPO)
 
 METRIC = "questions/sec reweighted-decode + heads/sec IE-sweep, Llama-3-8B NQ-1000"
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md; ~6300 achievable)
 PMC_FILE = os.path.join(REPO, "profiles", "attn_pmc.json")
+
+
+def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, iters=20):
+    """HBM roofline of the decode attention kernel at the decode leg's own shape (outside its timed region): a
+    DecodeSession is prefilled with the same prompts, then cram_attn_decode on layer 0 (its bias, head enable,
+    split count and workspace) is launched `iters` times and timed with HIP events on the launch stream.
+    Algorithmic bytes = the visible K and V rows (sum of the sequence lengths x Hkv x d x 2 tensors x 2 B)."""
+    import torch
+    from cram_amd import ops
+    from cram_amd.engine import DecodeSession
+    sp = eng.spec
+    sess = DecodeSession(eng, prompts, weights16, heads, new_tokens)
+    sess.prefill()
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn(sess.B, sp.num_heads, sp.head_dim, device=dev, generator=g).to(eng.dtype)
+    out = torch.empty_like(q)
+
+    def run():
+        ops.attn_decode(q, sess.k_cache[0], sess.v_cache[0], scale=eng.scale, seq_lens=sess.seq_lens,
+                        bias=sess.cb.bias, enable=sess.cb.enable[0], W=sess.cb.W, num_splits=sess.splits,
+                        workspace=sess.ws, out=out)
+
+    for _ in range(3):
+        run()
+    st = torch.cuda.current_stream(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(st)
+    for _ in range(iters):
+        run()
+    e.record(st)
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / iters
+    kv_bytes = float(sum(sess.lens)) * sp.num_kv_heads * sp.head_dim * 2 * 2
+    ach = kv_bytes / (ms * 1e-3) / 1e9
+    res = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "decode_kernel (+ decode_combine_kernel when split)",
+           "avg_launch_ms": round(ms, 4), "bytes_per_launch": kv_bytes, "batch": sess.B, "splits": sess.splits,
+           "note": "layer 0 of the decode leg's prefilled KV cache, timed apart from the decode leg"}
+    del sess
+    torch.cuda.empty_cache()
+    return res
 
 
 def log(*a):
@@ -242,7 +284,9 @@ def main():
                   "seconds": float(dt.item()), "repeats": reps,
                   "host_encode_ms_per_question": round(host_ms / B, 3),
                   "note": "packed varlen prefill + graph-replayed greedy steps, EOS ignored (random weights)"}
-        log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s (T mean {T_mean:.0f})")
+        decode["attention_roofline"] = decode_attention_roofline(eng, prompts, ws, heads, args.decode_tokens, dev)
+        log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s (T mean {T_mean:.0f}); decode attention "
+            f"{decode['attention_roofline']['achieved']:.0f} GB/s")
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1, config 3)
     cpu = None
