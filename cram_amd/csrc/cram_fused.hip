@@ -103,15 +103,17 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(const T* __restrict__ x, in
 }
 
 // one thread = 8 rotation pairs (i, i + d/2) of one head of one row.  SPLIT: the row's heads are q | k | v
-// (hq, then (heads - hq) / 2 each); q rotates in place, k rotates into kout and v is copied into vout, where
-// row r = b * T + t of the buffer lands at row kv_row0 + t of sequence b (batch stride kv_bs, row stride kv_rs):
-// the suffix K/V of the IE sweep go straight behind their shared prefix, with no separate copy pass
+// (hq, then (heads - hq) / 2 each); q rotates in place, k rotates into kout (and in place too if keep_k) and v is
+// copied into vout.  Destination of buffer row r: sequence b = r / T, row kv_row0 + r % T, or, with dst_b,
+// sequence dst_b[r], row kv_row0 + pos[r]; strides kv_bs (sequence), kv_hs (head), kv_rs (row).  The IE sweep's
+// suffix K/V go straight behind their shared prefix, the packed decode prefill's K/V straight into the cache.
 template <typename E, bool SPLIT>
 __global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t rs, int rows, int T, int heads,
                                                    int d, const E* __restrict__ cos_t,
                                                    const E* __restrict__ sin_t, int64_t tab_rs,
                                                    const int64_t* __restrict__ pos, int hq, E* __restrict__ kout,
-                                                   E* __restrict__ vout, int64_t kv_bs, int64_t kv_rs, int kv_row0) {
+                                                   E* __restrict__ vout, int64_t kv_bs, int64_t kv_hs, int64_t kv_rs,
+                                                   int kv_row0, const int64_t* __restrict__ dst_b, int keep_k) {
   using V8 = typename Vec<E>::x8;
   const unsigned half = (unsigned)d >> 1, vpp = half >> 3;  // vectors per half-row
   const unsigned gid = blockIdx.x * 256u + threadIdx.x;      // host guarantees rows*heads*vpp < 2^31
@@ -125,17 +127,21 @@ __global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t 
   const V8 x1 = *reinterpret_cast<const V8*>(base);
   const V8 x2 = *reinterpret_cast<const V8*>(base + half);
   E* dst = base;
+  E* dst2 = nullptr;                                         // second destination of a rotated k (keep_k)
   if (SPLIT && h >= (unsigned)hq) {
     const unsigned hkv = ((unsigned)heads - (unsigned)hq) >> 1;
     const bool is_v = h >= (unsigned)hq + hkv;
     const unsigned hk = h - (unsigned)hq - (is_v ? hkv : 0u);
-    const int64_t b = row32 / (unsigned)T, t = row32 % (unsigned)T;
-    dst = (is_v ? vout : kout) + b * kv_bs + (kv_row0 + t) * kv_rs + (int64_t)hk * d + vi * 8;
+    const int64_t b = dst_b ? dst_b[row] : (int64_t)(row32 / (unsigned)T);
+    const int64_t t = dst_b ? pos[row] : (int64_t)(row32 % (unsigned)T);
+    E* o = (is_v ? vout : kout) + b * kv_bs + (kv_row0 + t) * kv_rs + (int64_t)hk * kv_hs + vi * 8;
     if (is_v) {                                              // v: copied, not rotated
-      *reinterpret_cast<V8*>(dst) = x1;
-      *reinterpret_cast<V8*>(dst + half) = x2;
+      *reinterpret_cast<V8*>(o) = x1;
+      *reinterpret_cast<V8*>(o + half) = x2;
       return;
     }
+    if (keep_k) dst2 = o;
+    else dst = o;
   }
   const int64_t p = pos ? pos[row] : (int64_t)(row32 % (unsigned)T);
   const E* ct = cos_t + p * tab_rs + vi * 8;
@@ -152,6 +158,10 @@ __global__ __launch_bounds__(256) void rope_kernel(E* __restrict__ qkv, int64_t 
   }
   *reinterpret_cast<V8*>(dst) = o1;
   *reinterpret_cast<V8*>(dst + half) = o2;
+  if (SPLIT && dst2) {
+    *reinterpret_cast<V8*>(dst2) = o1;
+    *reinterpret_cast<V8*>(dst2 + half) = o2;
+  }
 }
 
 template <typename T>
@@ -226,23 +236,24 @@ int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads,
   const hipStream_t st = (hipStream_t)stream;
   if (dtype == CRAM_DTYPE_BF16)
     hipLaunchKernelGGL((rope_kernel<__bf16, false>), g, dim3(256), 0, st, (__bf16*)qkv, row_stride, rows, T, heads,
-                       d, (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos, heads, nullptr, nullptr, 0, 0, 0);
+                       d, (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos, heads, nullptr, nullptr, 0, 0, 0, 0, nullptr, 0);
   else
     hipLaunchKernelGGL((rope_kernel<_Float16, false>), g, dim3(256), 0, st, (_Float16*)qkv, row_stride, rows, T,
                        heads, d, (const _Float16*)cos_t, (const _Float16*)sin_t, tab_rs, pos, heads, nullptr, nullptr,
-                       0, 0, 0);
+                       0, 0, 0, 0, nullptr, 0);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 
 int cram_rope_split(void* qkv, int64_t row_stride, int rows, int T, int hq, int hkv, int d, const void* cos_t,
                     const void* sin_t, int64_t tab_rs, const int64_t* pos, void* kout, void* vout, int64_t kv_bs,
-                    int64_t kv_rs, int kv_row0, int dtype, cram_stream_t stream) {
+                    int64_t kv_hs, int64_t kv_rs, int kv_row0, const int64_t* dst_b, int keep_k, int dtype,
+                    cram_stream_t stream) {
   if (!qkv || !cos_t || !sin_t || !kout || !vout || rows < 0 || hq <= 0 || hkv <= 0 || T <= 0 || kv_row0 < 0 ||
-      rows % T != 0)
+      (dst_b ? !pos : rows % T != 0))
     return CRAM_ERR_INVALID_ARG;
   if (!dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
   if (rows == 0) return CRAM_OK;
-  if ((d & 15) || !m8(row_stride) || !m8(tab_rs) || !m8(kv_bs) || !m8(kv_rs) || !al16(qkv) || !al16(cos_t) ||
+  if ((d & 15) || !m8(row_stride) || !m8(tab_rs) || !m8(kv_bs) || !m8(kv_hs) || !m8(kv_rs) || !al16(qkv) || !al16(cos_t) ||
       !al16(sin_t) || !al16(kout) || !al16(vout))
     return CRAM_ERR_ALIGNMENT;
   const int heads = hq + 2 * hkv;
@@ -253,11 +264,11 @@ int cram_rope_split(void* qkv, int64_t row_stride, int rows, int T, int hq, int 
   if (dtype == CRAM_DTYPE_BF16)
     hipLaunchKernelGGL((rope_kernel<__bf16, true>), g, dim3(256), 0, st, (__bf16*)qkv, row_stride, rows, T, heads,
                        d, (const __bf16*)cos_t, (const __bf16*)sin_t, tab_rs, pos, hq, (__bf16*)kout, (__bf16*)vout,
-                       kv_bs, kv_rs, kv_row0);
+                       kv_bs, kv_hs, kv_rs, kv_row0, dst_b, keep_k);
   else
     hipLaunchKernelGGL((rope_kernel<_Float16, true>), g, dim3(256), 0, st, (_Float16*)qkv, row_stride, rows, T,
                        heads, d, (const _Float16*)cos_t, (const _Float16*)sin_t, tab_rs, pos, hq, (_Float16*)kout,
-                       (_Float16*)vout, kv_bs, kv_rs, kv_row0);
+                       (_Float16*)vout, kv_bs, kv_hs, kv_rs, kv_row0, dst_b, keep_k);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }
 

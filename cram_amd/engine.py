@@ -448,12 +448,14 @@ class DecodeSession:
                 h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
             y = ops.linear(x, lw.wqkv, lw.bqkv)
             yr = y[:total]
-            ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, self.cos, self.sin, T=1, pos=pos)
+            # q and k roped in place (the varlen attention reads them there), roped k and v also written straight
+            # into the cache rows (sequence bidx, position pos) of this layer
+            ops.rope_split(yr, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
+                           self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2), 0, pos=pos, dst_b=bidx,
+                           keep_k=True)
             q = yr[:, :sp.q_size].view(total, sp.num_heads, sp.head_dim)
             k = yr[:, sp.q_size:sp.q_size + sp.kv_size].view(total, sp.num_kv_heads, sp.head_dim)
             v = yr[:, sp.q_size + sp.kv_size:].view(total, sp.num_kv_heads, sp.head_dim)
-            self.k_cache[l, bidx, :, pos] = k
-            self.v_cache[l, bidx, :, pos] = v
             a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
             if Mp > total:
                 a[total:].zero_()

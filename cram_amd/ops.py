@@ -296,9 +296,13 @@ def rope_inplace(qkv: torch.Tensor, heads: int, head_dim: int, cos: torch.Tensor
 
 
 def rope_split(qkv: torch.Tensor, hq: int, hkv: int, head_dim: int, cos: torch.Tensor, sin: torch.Tensor, T: int,
-               kout: torch.Tensor, vout: torch.Tensor, row0: int, pos: Optional[torch.Tensor] = None) -> None:
-    """RoPE over a fused q | k | v row buffer of B*T rows: q rotated in place, k rotated into kout[b, row0 + t] and v
-    copied into vout[b, row0 + t] (kout/vout [B, S, hkv, head_dim], rows contiguous)."""
+               kout: torch.Tensor, vout: torch.Tensor, row0: int, pos: Optional[torch.Tensor] = None,
+               dst_b: Optional[torch.Tensor] = None, keep_k: bool = False) -> None:
+    """RoPE over a fused q | k | v row buffer: q rotated in place, k rotated into kout (and kept in place too if
+    ``keep_k``) and v copied into vout.  kout/vout are [B, S, hkv, head_dim] views with any strides (e.g. the
+    decode cache [B, hkv, S, d] transposed).  Buffer row r goes to kout[r // T, row0 + r % T] (B * T rows), or,
+    with ``dst_b`` (int64 per row, device), to kout[dst_b[r], row0 + pos[r]]: the caller guarantees
+    dst_b < B and row0 + pos < S."""
     y2 = _rows2d(qkv, "qkv")
     dt = _dt(qkv)
     rows = y2.shape[0]
@@ -306,16 +310,21 @@ def rope_split(qkv: torch.Tensor, hq: int, hkv: int, head_dim: int, cos: torch.T
         raise ValueError("cos/sin must be [P, d] tables of the QKV buffer's dtype")
     if pos is not None and (pos.dtype != torch.int64 or pos.numel() != rows):
         raise ValueError("pos must be int64 with one entry per row")
+    if dst_b is not None and (pos is None or dst_b.dtype != torch.int64 or dst_b.numel() != rows
+                              or dst_b.device != qkv.device):
+        raise ValueError("dst_b needs pos and must be a device int64 tensor with one entry per row")
     for t in (kout, vout):
-        if (t.dtype != qkv.dtype or t.device != qkv.device or t.dim() != 4 or t.shape[2:] != (hkv, head_dim)
-                or t.stride(3) != 1 or t.stride(2) != head_dim or t.shape[0] * T != rows or row0 + T > t.shape[1]):
-            raise ValueError("kout/vout must be [B, S >= row0 + T, hkv, head_dim] with contiguous rows, B * T rows")
-    if kout.stride()[:2] != vout.stride()[:2]:
-        raise ValueError("kout and vout must share their batch and row strides")
+        if (t.dtype != qkv.dtype or t.device != qkv.device or t.dim() != 4 or tuple(t.shape[2:]) != (hkv, head_dim)
+                or t.stride(3) != 1):
+            raise ValueError("kout/vout must be [B, S, hkv, head_dim] views with a contiguous last dimension")
+        if dst_b is None and (t.shape[0] * T != rows or row0 + T > t.shape[1]):
+            raise ValueError("kout/vout must hold B = rows / T sequences of at least row0 + T rows")
+    if kout.stride()[:3] != vout.stride()[:3]:
+        raise ValueError("kout and vout must share their strides")
     code = _lib.load().cram_rope_split(y2.data_ptr(), y2.stride(0), rows, int(T), int(hq), int(hkv), int(head_dim),
                                        cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), kout.data_ptr(),
-                                       vout.data_ptr(), kout.stride(0), kout.stride(1), int(row0), dt,
-                                       _stream(qkv.device))
+                                       vout.data_ptr(), kout.stride(0), kout.stride(2), kout.stride(1), int(row0),
+                                       _ptr(dst_b), int(bool(keep_k)), dt, _stream(qkv.device))
     _lib.check(code, "cram_rope_split")
 
 

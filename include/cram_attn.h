@@ -133,9 +133,11 @@ int cram_answer_logits(const void* hidden, int64_t h_rs, const void* w_lm, int64
  *                    place; row r uses position pos[r] (int64) or r % T when pos == NULL; cos/sin are
  *                    [P][d] tables of the same dtype (row stride tab_rs).
  * cram_rope_split    the same rotation over a q | k | v row (hq, hkv, hkv heads): q in place, k rotated into
- *                    kout and v copied into vout, buffer row r = b * T + t going to row kv_row0 + t of sequence
- *                    b (batch stride kv_bs, row stride kv_rs, elements): the IE sweep's suffix K/V written
- *                    behind their shared prefix (cram_amd/engine.py layer_rows) with no copy pass; rows % T == 0
+ *                    kout (and also in place when keep_k) and v copied into vout.  Buffer row r goes to row
+ *                    kv_row0 + r % T of sequence r / T (rows % T == 0), or, when dst_b is given, to row
+ *                    kv_row0 + pos[r] of sequence dst_b[r] (int64); element strides kv_bs (sequence), kv_hs
+ *                    (head), kv_rs (row).  Replaces the copies / index_put that placed the IE sweep's suffix K/V
+ *                    behind their prefix and the packed decode prefill's K/V into the cache (cram_amd/engine.py)
  * cram_silu_mul      y[r, :F] = rnd(rnd(silu(gu[r, :F])) * gu[r, F:2F])
  */
 int cram_rmsnorm(const void* x, int64_t x_rs, const void* residual, int64_t r_rs, void* h_out, int64_t h_rs,
@@ -145,7 +147,8 @@ int cram_rope_inplace(void* qkv, int64_t row_stride, int rows, int T, int heads,
                       const void* sin_t, int64_t tab_rs, const int64_t* pos, int dtype, cram_stream_t stream);
 int cram_rope_split(void* qkv, int64_t row_stride, int rows, int T, int hq, int hkv, int d, const void* cos_t,
                     const void* sin_t, int64_t tab_rs, const int64_t* pos, void* kout, void* vout, int64_t kv_bs,
-                    int64_t kv_rs, int kv_row0, int dtype, cram_stream_t stream);
+                    int64_t kv_hs, int64_t kv_rs, int kv_row0, const int64_t* dst_b, int keep_k, int dtype,
+                    cram_stream_t stream);
 int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows, int F, int dtype,
                   cram_stream_t stream);
 

@@ -101,14 +101,22 @@ def rope_inplace(qkv, heads, head_dim, cos, sin, T, pos=None):
     return qkv
 
 
-def rope_split(qkv, hq, hkv, head_dim, cos, sin, T, kout, vout, row0, pos=None):
+def rope_split(qkv, hq, hkv, head_dim, cos, sin, T, kout, vout, row0, pos=None, dst_b=None, keep_k=False):
     y = qkv.reshape(-1, qkv.shape[-1])
+    q_size, kv = hq * head_dim, hkv * head_dim
+    k_raw = y[:, q_size:q_size + kv].clone()
     rope_inplace(y, hq + hkv, head_dim, cos, sin, T, pos)
-    B = y.shape[0] // T
-    kv = hkv * head_dim
-    q_size = hq * head_dim
-    kout[:, row0:row0 + T] = y[:, q_size:q_size + kv].reshape(B, T, hkv, head_dim)
-    vout[:, row0:row0 + T] = y[:, q_size + kv:q_size + 2 * kv].reshape(B, T, hkv, head_dim)
+    k_rot = y[:, q_size:q_size + kv].reshape(-1, hkv, head_dim)
+    v = y[:, q_size + kv:q_size + 2 * kv].reshape(-1, hkv, head_dim)
+    if dst_b is None:
+        B = y.shape[0] // T
+        kout[:, row0:row0 + T] = k_rot.reshape(B, T, hkv, head_dim)
+        vout[:, row0:row0 + T] = v.reshape(B, T, hkv, head_dim)
+    else:
+        kout[dst_b, row0 + pos] = k_rot
+        vout[dst_b, row0 + pos] = v
+    if not keep_k:
+        y[:, q_size:q_size + kv] = k_raw
 
 
 def silu_mul(gu, F, out=None):

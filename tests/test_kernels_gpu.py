@@ -234,6 +234,37 @@ def test_rope_split_equals_inplace_plus_copy(gpu_device, Hq, Hkv, dtype):
     assert torch.equal(ybuf[B * T:], pad_before)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_rope_split_scatter_into_cache(gpu_device, dtype):
+    """The packed decode prefill's form of cram_rope_split: q and k roped in place (keep_k), and the roped k / the v
+    of packed row r written to cache row pos[r] of sequence dst_b[r] in the head-major [B, Hkv, S, d] cache, bit-
+    identical to rope_inplace followed by the index_put it replaces; untouched cache rows stay as they were."""
+    from cram_amd import ops
+    from cram_amd.engine import CrAMEngine, ModelSpec
+    dev = gpu_device
+    Hq, Hkv, d = 32, 8, 128
+    sp = ModelSpec(1, Hq * d, Hq, Hkv, d, 256, 100, 1e-5, False)
+    eng = CrAMEngine.random(sp, dev, seed=2, dtype=dtype)
+    B, S = 6, 200
+    lens = [37, 1, 120, 64, 5, 90]
+    pos = torch.cat([torch.arange(n) for n in lens]).to(dev)
+    bidx = torch.cat([torch.full((n,), b) for b, n in enumerate(lens)]).to(dev)
+    total, N = sum(lens), (Hq + 2 * Hkv) * d
+    cos, sin = eng.rope_tables(S)
+    y = torch.randn(total, N, device=dev).to(dtype)
+    y_ref = y.clone()
+    ops.rope_inplace(y_ref, Hq + Hkv, d, cos, sin, 1, pos=pos)
+    kc = torch.randn(B, Hkv, S, d, device=dev).to(dtype)
+    vc = torch.randn_like(kc)
+    kc_ref, vc_ref = kc.clone(), vc.clone()
+    kc_ref[bidx, :, pos] = y_ref[:, Hq * d:(Hq + Hkv) * d].view(total, Hkv, d)
+    vc_ref[bidx, :, pos] = y_ref[:, (Hq + Hkv) * d:].view(total, Hkv, d)
+    ops.rope_split(y, Hq, Hkv, d, cos, sin, 1, kc.transpose(1, 2), vc.transpose(1, 2), 0, pos=pos, dst_b=bidx,
+                   keep_k=True)
+    assert torch.equal(y, y_ref)
+    assert torch.equal(kc, kc_ref) and torch.equal(vc, vc_ref)
+
+
 @pytest.mark.parametrize("F", [512, 14336, 18944])
 def test_silu_mul_matches_transformers(gpu_device, F):
     from cram_amd import ops
