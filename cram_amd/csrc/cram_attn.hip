@@ -531,12 +531,11 @@ struct DecodeParams {
   float* ws_ml;  // [B][Hq][nsplit][2]  partial (max, sum)
 };
 
-template <typename T, int D, int G>
+template <typename T, int D, int G, int U = 4>   // U: keys per lane group per iteration
 __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
   using V8 = typename Vec<T>::x8;
   constexpr int LPK = D / 8;        // lanes per key row (8 elements = 16 B per lane)
   constexpr int KPW = 64 / LPK;     // keys per wave-instruction
-  constexpr int U = 4;              // keys per lane group per iteration
   constexpr int STEP = 4 * KPW;     // keys per workgroup per unrolled slot
   __shared__ float red_m[4][G], red_l[4][G];
   __shared__ float red_o[4][G][D];
@@ -773,7 +772,19 @@ int dispatch_prefill(PrefillParams& p, int d, int dtype, hipStream_t stream) {
 
 template <typename T, int D, int G>
 int launch_decode_g(DecodeParams& p, int nsplit, hipStream_t stream) {
-  hipLaunchKernelGGL((decode_kernel<T, D, G>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+  // keys per lane group per iteration: with >= 1024 workgroups (e.g. the batch-256 decode leg) occupancy is what
+  // keeps K/V reads in flight, and U = 2 (149 VGPRs, three waves per SIMD) read 4.43 vs 4.12 TB/s for U = 4 (205
+  // VGPRs, two waves; tools/ab_decode_u.py); smaller grids keep U = 4's deeper per-wave prefetch.
+  // CRAM_DECODE_U = 2 | 4 | 8 overrides (A/B)
+  int u = (int64_t)p.Hkv * p.B * nsplit >= 1024 ? 2 : 4;
+  const char* eu = getenv("CRAM_DECODE_U");
+  if (eu && (eu[0] == '2' || eu[0] == '4' || eu[0] == '8')) u = eu[0] - '0';
+  if (u == 8)
+    hipLaunchKernelGGL((decode_kernel<T, D, G, 8>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+  else if (u == 2)
+    hipLaunchKernelGGL((decode_kernel<T, D, G, 2>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+  else
+    hipLaunchKernelGGL((decode_kernel<T, D, G>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
   if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
   if (nsplit > 1) {
     hipLaunchKernelGGL((decode_combine_kernel<T, D>), dim3(p.Hq, p.B), dim3(D), 0, stream, p, nsplit);

@@ -33,3 +33,14 @@ def prefill_variant(request, monkeypatch):
     else:
         monkeypatch.delenv("CRAM_PREFILL_VARIANT", raising=False)
     return request.param
+
+
+@pytest.fixture(params=["auto", "u2", "u8"])
+def decode_variant(request, monkeypatch):
+    """Run a decode test on every decode_kernel instantiation: the size-picked keys-per-iteration U (2 for grids of
+    >= 1024 workgroups, else 4) and the forced U = 2 / 8 (CRAM_DECODE_U, read at every launch)."""
+    if request.param == "auto":
+        monkeypatch.delenv("CRAM_DECODE_U", raising=False)
+    else:
+        monkeypatch.setenv("CRAM_DECODE_U", request.param[1])
+    return request.param

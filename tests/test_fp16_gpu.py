@@ -82,7 +82,7 @@ def test_prefill_fp16_zero_bias_is_no_bias(gpu_device, prefill_variant):
 
 
 @pytest.mark.parametrize("B,Hq,Hkv,S,splits", [(2, 40, 40, 700, 1), (3, 40, 40, 1500, 4), (2, 8, 2, 333, 2)])
-def test_decode_fp16(gpu_device, B, Hq, Hkv, S, splits):
+def test_decode_fp16(gpu_device, decode_variant, B, Hq, Hkv, S, splits):
     from cram_amd import ops
     d = 128
     gen = torch.Generator().manual_seed(S + splits)

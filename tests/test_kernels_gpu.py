@@ -90,7 +90,7 @@ def test_prefill_query_offset(gpu_device, prefill_variant):
     (2, 4, 4, 513, 128, 1), (1, 16, 2, 2049, 128, 8), (2, 8, 4, 300, 64, 2), (1, 8, 1, 64, 128, 2),
 ])
 @pytest.mark.parametrize("ragged", [False, True])
-def test_decode_matches_oracle(gpu_device, B, Hq, Hkv, S, d, splits, ragged):
+def test_decode_matches_oracle(gpu_device, decode_variant, B, Hq, Hkv, S, d, splits, ragged):
     gen = torch.Generator().manual_seed(S * 31 + Hq + splits + ragged)
     q = torch.randn(B, Hq, d, generator=gen).to(torch.bfloat16)
     k = torch.randn(B, Hkv, S + 5, d, generator=gen).to(torch.bfloat16)   # padded cache (S_max > S)
