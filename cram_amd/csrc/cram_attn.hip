@@ -773,14 +773,15 @@ int dispatch_prefill(PrefillParams& p, int d, int dtype, hipStream_t stream) {
 template <typename T, int D, int G>
 int launch_decode_g(DecodeParams& p, int nsplit, hipStream_t stream) {
   // keys per lane group per iteration: with >= 1024 workgroups (e.g. the batch-256 decode leg) occupancy is what
-  // keeps K/V reads in flight, and U = 2 (149 VGPRs, three waves per SIMD) read 4.43 vs 4.12 TB/s for U = 4 (205
-  // VGPRs, two waves; tools/ab_decode_u.py); smaller grids keep U = 4's deeper per-wave prefetch.
-  // CRAM_DECODE_U = 2 | 4 | 8 overrides (A/B)
-  int u = (int64_t)p.Hkv * p.B * nsplit >= 1024 ? 2 : 4;
+  // keeps K/V reads in flight: U = 1 (114 VGPRs, four waves per SIMD) read 4.73 TB/s, U = 2 (149, three) 4.56,
+  // U = 4 (205, two) 4.12 (tools/ab_decode_u.py, B = 256); at 512 workgroups U = 4's deeper per-wave prefetch
+  // wins (4.32 vs 4.01 for U = 1).  CRAM_DECODE_U = 1 | 2 | 4 overrides (A/B, tests)
+  // (G <= 4 only: the G = 7 Qwen2 body does 7/4 the VALU work per byte and ran 2.40 vs 2.96 TB/s with U = 1)
+  int u = (G <= 4 && (int64_t)p.Hkv * p.B * nsplit >= 1024) ? 1 : 4;
   const char* eu = getenv("CRAM_DECODE_U");
-  if (eu && (eu[0] == '2' || eu[0] == '4' || eu[0] == '8')) u = eu[0] - '0';
-  if (u == 8)
-    hipLaunchKernelGGL((decode_kernel<T, D, G, 8>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+  if (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) u = eu[0] - '0';
+  if (u == 1)
+    hipLaunchKernelGGL((decode_kernel<T, D, G, 1>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
   else if (u == 2)
     hipLaunchKernelGGL((decode_kernel<T, D, G, 2>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
   else

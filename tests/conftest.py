@@ -35,10 +35,10 @@ def prefill_variant(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(params=["auto", "u2", "u8"])
+@pytest.fixture(params=["auto", "u1", "u2"])
 def decode_variant(request, monkeypatch):
-    """Run a decode test on every decode_kernel instantiation: the size-picked keys-per-iteration U (2 for grids of
-    >= 1024 workgroups, else 4) and the forced U = 2 / 8 (CRAM_DECODE_U, read at every launch)."""
+    """Run a decode test on every decode_kernel instantiation: the size-picked keys-per-iteration U (1 for grids of
+    >= 1024 workgroups, else 4) and the forced U = 1 / 2 (CRAM_DECODE_U, read at every launch)."""
     if request.param == "auto":
         monkeypatch.delenv("CRAM_DECODE_U", raising=False)
     else:

@@ -29,7 +29,7 @@ out = torch.empty_like(q)
 ref = None
 res = {}
 for rnd in range(5):
-    for u in ("4", "2", "8"):
+    for u in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("4", "2", "1")):
         os.environ["CRAM_DECODE_U"] = u
         run = lambda: ops.attn_decode(q, kc, vc, scale=d ** -0.5, seq_lens=lens, bias=bias, enable=enable, W=S,
                                       out=out)
