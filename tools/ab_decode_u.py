@@ -1,7 +1,7 @@
 """Same-process A/B of decode_kernel's keys-per-iteration U (CRAM_DECODE_U, read at every launch) at the decode
 leg's shape (B sequences of ragged length, Llama-3 GQA 4:1, credibility bias on half the heads).
 
-    python tools/ab_decode_u.py [B] [S]
+    [AB_HEADS=Hq,Hkv,d] python tools/ab_decode_u.py [B] [S] [U list, e.g. 4,2,1]
 """
 import os
 import statistics
@@ -14,7 +14,7 @@ from cram_amd import ops  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-Hq, Hkv, d = 32, 8, 128
+Hq, Hkv, d = (int(x) for x in os.environ.get("AB_HEADS", "32,8,128").split(","))
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 kc = torch.randn(B, Hkv, S, d, device=dev, generator=g).to(torch.bfloat16)
