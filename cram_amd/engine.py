@@ -469,14 +469,17 @@ class DecodeSession:
         self.tokens[b0:b1] = self._pick(ops.linear(hn, eng.lm_head))
 
     def _step_body(self):
-        eng = self.eng
+        eng, sp = self.eng, self.eng.spec
         h = eng.embed[self.tokens][:, None]                      # [B, 1, D]
         self.seq_lens.add_(1)
         for l, lw in enumerate(eng.layers):
             x = eng.rmsnorm(h, lw.ln1)
-            q, k, v = eng.qkv(x, lw, self.cos, self.sin, pos=self.pos)
-            self.k_cache[l, self.rows, :, self.pos] = k[:, 0]
-            self.v_cache[l, self.rows, :, self.pos] = v[:, 0]
+            y = ops.linear(x, lw.wqkv, lw.bqkv)                # [B, 1, (Hq + 2 Hkv) d]
+            # q roped in place; the new token's roped k and its v straight into cache row pos of every sequence
+            ops.rope_split(y, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
+                           self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2), 0, pos=self.pos,
+                           dst_b=self.rows)
+            q = y[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
             a = ops.attn_decode(q[:, 0], self.k_cache[l], self.v_cache[l], scale=eng.scale, seq_lens=self.seq_lens,
                                 bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
                                 workspace=self.ws)
