@@ -262,7 +262,7 @@ class CrAMEngine:
     def layer_rows(self, hbuf: torch.Tensor, B: int, T: int, l: int, cos, sin, bias=None, enable=None, W: int = 0,
                    out_rows: Optional[int] = None, delta: Optional[torch.Tensor] = None, prefix=None):
         """One decoder layer over a ROW buffer: rows [0, B*T) are B sequences of T tokens, rows beyond are
-        alignment padding (GEMM M rounded up to the 256-row hipBLASLt/rocBLAS macro tile; padding rows carry
+        alignment padding (GEMM M from padded_rows: the 256-row macro tile, then the measured row table; padding rows carry
         garbage and are never read back).  The layer input is hbuf [Mp, D], or hbuf + delta when the previous
         layer's MLP output is still pending (the residual add then runs inside this layer's first RMSNorm).
         Returns (h, mlp_out): the layer output is h + mlp_out, left for the next consumer to fuse.

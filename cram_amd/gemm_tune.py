@@ -67,7 +67,7 @@ def install(m_values: Iterable[int], dtype: str = "BFloat16", path: str = SOLUTI
 
 
 def sweep_rows(lo: int = 8192, hi: int = 65536, step: int = 256) -> Tuple[int, ...]:
-    """Row counts the sweep's suffix batches (33 x T, rounded up to 256) and the packed prefill chunks take."""
+    """Row counts the sweep's suffix batches (33 x T, padded_rows) and the packed prefill chunks take: multiples of 256."""
     return tuple(range(lo, hi + 1, step))
 
 
