@@ -17,12 +17,14 @@ _c_int32_p = POINTER(ctypes.c_int32)
 _c_uint8_p = POINTER(ctypes.c_uint8)
 _c_float_p = POINTER(c_float)
 
-ABI_VERSION = 2   # CRAM_ABI_VERSION of include/cram_attn.h
+ABI_VERSION = 3   # CRAM_ABI_VERSION of include/cram_attn.h
 
 # name -> (restype, argtypes); the exact export list of include/cram_attn.h
 SIGNATURES = {
     "cram_strerror": (ctypes.c_char_p, [c_int]),
     "cram_abi_version": (c_int, []),
+    "cram_set_knob": (c_int, [c_int, c_int]),
+    "cram_get_knob": (c_int, [c_int]),
     "cram_attn_prefill": (c_int, [
         c_void_p, c_int64, c_int64, c_int64,
         c_void_p, c_int64, c_int64, c_int64,
@@ -98,3 +100,15 @@ def check(code: int, what: str) -> None:
     if code != 0:
         msg = load().cram_strerror(code).decode()
         raise RuntimeError(f"{what} failed: CRAM error {code} ({msg})")
+
+
+KNOB_PREFILL_VARIANT = 0   # CRAM_KNOB_PREFILL_VARIANT
+KNOB_DECODE_U = 1          # CRAM_KNOB_DECODE_U
+
+
+def set_knob(which: int, value: int) -> int:
+    """Set a process-wide kernel-selection knob (-1 = automatic); returns the previous value."""
+    lib = load()
+    prev = lib.cram_get_knob(which)
+    check(lib.cram_set_knob(which, int(value)), "cram_set_knob")
+    return prev

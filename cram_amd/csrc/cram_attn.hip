@@ -736,6 +736,24 @@ __global__ __launch_bounds__(256) void answer_logits_kernel(const T* h, int64_t 
 // --------------------------------------------------------------------------------------------
 // host helpers
 // --------------------------------------------------------------------------------------------
+// Process-wide kernel selection knobs (cram_set_knob): -1 = automatic.  The environment is read ONCE, at the
+// first query, as the initial value (CRAM_PREFILL_VARIANT = 3 | 8, CRAM_DECODE_U = 1 | 2 | 4); launches never
+// call getenv.  A knob changed after a hipGraph capture does not alter the captured launches.
+int g_knob[CRAM_KNOB_COUNT];
+bool g_knob_init = false;
+inline void knobs_init() {
+  if (g_knob_init) return;
+  const char* e = getenv("CRAM_PREFILL_VARIANT");
+  g_knob[CRAM_KNOB_PREFILL_VARIANT] = (e && (e[0] == '3' || e[0] == '8')) ? e[0] - '0' : -1;
+  const char* eu = getenv("CRAM_DECODE_U");
+  g_knob[CRAM_KNOB_DECODE_U] = (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1;
+  g_knob_init = true;
+}
+inline int knob(int k) {
+  knobs_init();
+  return g_knob[k];
+}
+
 inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
 inline bool m8(int64_t s) { return (s & 7) == 0; }
 
@@ -743,12 +761,12 @@ template <typename T, int D>
 int launch_prefill(PrefillParams& p, hipStream_t stream) {
   const int G = p.Hq / p.Hkv;
   p.hp = (G % 4 == 0) ? 4 : (G % 2 == 0) ? 2 : 1;
-  // CRAM_PREFILL_VARIANT=3 (opt-in): 32-key tiles, 162 VGPRs -> three waves per SIMD; +4 % at the sweep
+  // variant 3 (opt-in, knob CRAM_KNOB_PREFILL_VARIANT / env CRAM_PREFILL_VARIANT=3): 32-key tiles, 162 VGPRs -> three waves per SIMD; +4 % at the sweep
   // shape, but on the tiny Qwen2 model its IE noise doubled on one question and broke the parity bar
   // (tools/ie_noise_probe.py), so 64-key tiles at two waves per SIMD stay the default.
-  // CRAM_PREFILL_VARIANT=8: 8-wave workgroups (one per CU), every K/V tile feeds twice the query rows.
-  const char* e = getenv("CRAM_PREFILL_VARIANT");
-  const int var = (D == 128 && e && (e[0] == '3' || e[0] == '8')) ? e[0] - '0' : 0;
+  // variant 8: 8-wave workgroups (one per CU), every K/V tile feeds twice the query rows.
+  const int kv = knob(CRAM_KNOB_PREFILL_VARIANT);
+  const int var = (D == 128 && (kv == 3 || kv == 8)) ? kv : 0;
   const int nw = var == 8 ? 8 : 4;
   const int bq = 32 * (nw / p.hp);
   p.nqb = (p.Tq + bq - 1) / bq;
@@ -775,11 +793,11 @@ int launch_decode_g(DecodeParams& p, int nsplit, hipStream_t stream) {
   // keys per lane group per iteration: with >= 1024 workgroups (e.g. the batch-256 decode leg) occupancy is what
   // keeps K/V reads in flight: U = 1 (114 VGPRs, four waves per SIMD) read 4.73 TB/s, U = 2 (149, three) 4.56,
   // U = 4 (205, two) 4.12 (tools/ab_decode_u.py, B = 256); at 512 workgroups U = 4's deeper per-wave prefetch
-  // wins (4.32 vs 4.01 for U = 1).  CRAM_DECODE_U = 1 | 2 | 4 overrides (A/B, tests)
+  // wins (4.32 vs 4.01 for U = 1).  The knob CRAM_KNOB_DECODE_U = 1 | 2 | 4 overrides (A/B, tests)
   // (G <= 4 only: the G = 7 Qwen2 body does 7/4 the VALU work per byte and ran 2.40 vs 2.96 TB/s with U = 1)
   int u = (G <= 4 && (int64_t)p.Hkv * p.B * nsplit >= 1024) ? 1 : 4;
-  const char* eu = getenv("CRAM_DECODE_U");
-  if (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) u = eu[0] - '0';
+  const int ku = knob(CRAM_KNOB_DECODE_U);
+  if (ku == 1 || ku == 2 || ku == 4) u = ku;
   if (u == 1)
     hipLaunchKernelGGL((decode_kernel<T, D, G, 1>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
   else if (u == 2)
@@ -825,6 +843,22 @@ const char* cram_strerror(int code) {
 }
 
 int cram_abi_version(void) { return CRAM_ABI_VERSION; }
+
+int cram_set_knob(int which, int value) {
+  if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
+  knobs_init();
+  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 8)
+    return CRAM_ERR_INVALID_ARG;
+  if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
+    return CRAM_ERR_INVALID_ARG;
+  g_knob[which] = value;
+  return CRAM_OK;
+}
+
+int cram_get_knob(int which) {
+  if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
+  return knob(which);
+}
 
 int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sb,
                       int64_t k_sh, int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st, void* o,

@@ -1,7 +1,8 @@
 """IE-sweep drivers and influential-head ranking (utils/find_best_heads.py, same file formats).
 
   casual_tracing_per_head       find_best_heads.py:13-58   per-question IE grid, resume by skipping
-  casual_tracing_per_head_with_position  :61-110          fake passage moved through positions 0..4
+  casual_tracing_per_head_with_position  :61-110          fake passage moved through positions 0..4,
+                                                           heads_scores_pos.json rewritten per question (+resume)
   casual_tracing_combine_all    :113-132                   mean over questions, ranking
   find_top_k_heads              :135-150                   top-k -> {layer: [heads]}
 
@@ -83,22 +84,59 @@ def casual_tracing_per_head(data: list, model, output_file: str, contexts_type=(
         wrong = sample.get("wrong answer", sample.get("wrong_answer"))
         done.append(model.cal_logits(question=sample["question"], paras=ctx, scores=sc, wrong_answer=wrong))
         os.makedirs(os.path.dirname(os.path.abspath(output_file)), exist_ok=True)
-        with open(output_file, "w", encoding="utf-8") as f:
+        tmp = output_file + ".tmp"
+        with open(tmp, "w", encoding="utf-8") as f:
             json.dump(done, f, ensure_ascii=False, indent=4)
+        os.replace(tmp, output_file)
     return done
 
 
-def casual_tracing_per_head_with_position(data: list, model, topk: int = 4) -> list:
-    """find_best_heads.py:61-110: the fake passage at positions 0..4 among the 4 retrieved ones."""
-    res = []
-    for sample in data:
-        fake = sample["ori_fake"]
-        docs = sample["reranked_dense_ctxs"][:topk]
+def position_contexts(sample: dict, position: int, contexts_type=("ori_fake", "reranked_dense"), topk: int = 4):
+    """find_best_heads.py:83-99: the retrieved passages before `position`, then the fake passage(s), then the rest.
+
+    Quirk kept: every "ori_fake" passage is inserted but ONE score 0 is appended (:93-94), as in the plain sweep;
+    the retrieved passages always get [1] * position and [1] * (4 - position) (:89, :99), whatever topk is."""
+    docs = sample["reranked_dense_ctxs"][:topk]
+    contexts, scores = [], []
+    if "reranked_dense" in contexts_type:
+        contexts.extend(docs[:position])
+        scores.extend([1] * position)
+    if "ori_fake" in contexts_type:
+        contexts.extend(sample["ori_fake"])
+        scores.append(0)
+    if "reranked_dense" in contexts_type:
+        contexts.extend(docs[position:])
+        scores.extend([1] * (4 - position))
+    return contexts, scores
+
+
+def casual_tracing_per_head_with_position(data: list, model, output_file: str = None,
+                                          contexts_type=("ori_fake", "reranked_dense"), topk: int = 4,
+                                          resume: bool = True) -> list:
+    """find_best_heads.py:61-110: per question, the IE grid with the fake passage at positions 0..4 among the
+    retrieved ones -> [Nq][5][L][H].
+
+    Like the reference, the whole list is rewritten to `output_file` (heads_scores_pos.json) after every
+    question (:105-110).  Added: with resume=True the questions already in the file are skipped (the reference
+    restarts from [] on every run, :76, losing 5 x L x H units per finished question when a run dies); a
+    question is written only once all five positions are done, so a partial question is recomputed."""
+    done = []
+    if output_file and resume and os.path.exists(output_file):
+        with open(output_file, encoding="utf-8") as f:
+            done = json.load(f)
+    for idx, sample in enumerate(data):
+        if idx < len(done):
+            continue
         wrong = sample.get("wrong answer", sample.get("wrong_answer"))
         per_pos = []
-        for pos in range(5):
-            ctx = docs[:pos] + list(fake) + docs[pos:]
-            sc = [1] * pos + [0] + [1] * (4 - pos)
+        for position in range(5):
+            ctx, sc = position_contexts(sample, position, contexts_type, topk)
             per_pos.append(model.cal_logits(question=sample["question"], paras=ctx, scores=sc, wrong_answer=wrong))
-        res.append(per_pos)
-    return res
+        done.append(per_pos)
+        if output_file:
+            os.makedirs(os.path.dirname(os.path.abspath(output_file)), exist_ok=True)
+            tmp = output_file + ".tmp"
+            with open(tmp, "w", encoding="utf-8") as f:
+                json.dump(done, f, ensure_ascii=False, indent=4)
+            os.replace(tmp, output_file)          # a kill mid-write leaves the previous complete file
+    return done

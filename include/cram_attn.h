@@ -48,7 +48,7 @@ extern "C" {
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
 
-#define CRAM_ABI_VERSION 2        /* 2: dtype argument on every tensor entry point */
+#define CRAM_ABI_VERSION 3        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -57,6 +57,20 @@ typedef void* cram_stream_t; /* hipStream_t */
 
 const char* cram_strerror(int code);
 int cram_abi_version(void);
+
+/*
+ * Process-wide kernel-selection knobs (A/B runs and tests; the product default is automatic = -1).
+ * The initial values are read once from the environment (CRAM_PREFILL_VARIANT, CRAM_DECODE_U) at the first
+ * query; no launch reads the environment.  Not synchronised: set knobs before launching from other threads.
+ *   CRAM_KNOB_PREFILL_VARIANT  -1 / 0 = 64-key tiles, 4 waves (default); 3 = 32-key tiles; 8 = 8-wave workgroups
+ *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration
+ * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob returns the value.
+ */
+#define CRAM_KNOB_PREFILL_VARIANT 0
+#define CRAM_KNOB_DECODE_U 1
+#define CRAM_KNOB_COUNT 2
+int cram_set_knob(int which, int value);
+int cram_get_knob(int which);
 
 /*
  * Prefill / multi-token attention (replaces the hooked SDPA call for

@@ -24,23 +24,21 @@ def gpu_device():
 
 
 @pytest.fixture(params=["bk64", "bk32", "w8"])
-def prefill_variant(request, monkeypatch):
+def prefill_variant(request):
     """Run a prefill test on every d=128 prefill kernel: the default 64-key tiles at two waves per SIMD, the
-    opt-in 32-key tiles at three (CRAM_PREFILL_VARIANT=3) and the 8-wave workgroups (=8).  The library reads
-    the variable at every launch."""
-    if request.param in ("bk32", "w8"):
-        monkeypatch.setenv("CRAM_PREFILL_VARIANT", {"bk32": "3", "w8": "8"}[request.param])
-    else:
-        monkeypatch.delenv("CRAM_PREFILL_VARIANT", raising=False)
-    return request.param
+    opt-in 32-key tiles at three (variant 3) and the 8-wave workgroups (variant 8), selected through the
+    library's process-wide knob (cram_set_knob)."""
+    from cram_amd import _lib
+    prev = _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, {"bk64": -1, "bk32": 3, "w8": 8}[request.param])
+    yield request.param
+    _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, prev)
 
 
 @pytest.fixture(params=["auto", "u1", "u2"])
-def decode_variant(request, monkeypatch):
+def decode_variant(request):
     """Run a decode test on every decode_kernel instantiation: the size-picked keys-per-iteration U (1 for grids of
-    >= 1024 workgroups, else 4) and the forced U = 1 / 2 (CRAM_DECODE_U, read at every launch)."""
-    if request.param == "auto":
-        monkeypatch.delenv("CRAM_DECODE_U", raising=False)
-    else:
-        monkeypatch.setenv("CRAM_DECODE_U", request.param[1])
-    return request.param
+    >= 1024 workgroups, else 4) and the forced U = 1 / 2 (knob CRAM_KNOB_DECODE_U)."""
+    from cram_amd import _lib
+    prev = _lib.set_knob(_lib.KNOB_DECODE_U, -1 if request.param == "auto" else int(request.param[1]))
+    yield request.param
+    _lib.set_knob(_lib.KNOB_DECODE_U, prev)

@@ -29,7 +29,7 @@ def test_library_builds_loads_and_exports_every_symbol():
         assert hasattr(lib, n), n
     assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
     L = _lib.load()
-    assert L.cram_abi_version() == _lib.ABI_VERSION == 2
+    assert L.cram_abi_version() == _lib.ABI_VERSION == 3
     assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0
@@ -58,6 +58,22 @@ def test_argument_validation_without_gpu():
                               1, 1, 1, 4, None, 128, 1.0, None, 0, None, 0, 0, 4, None, 0, 0, None) == -5
     assert L.cram_rmsnorm(None, 0, None, 0, None, 0, None, None, 0, 1, 8, 1e-5, 0, None) == -1
     assert L.cram_silu_mul(fake, 8, fake, 8, 1, 12, 0, None) == -3
+
+
+def test_kernel_knobs_latch_without_gpu():
+    """Kernel selection is a process-wide knob (read from the environment once, never per launch)."""
+    from cram_amd import _lib
+    L = _lib.load()
+    prev = _lib.set_knob(_lib.KNOB_DECODE_U, 2)
+    try:
+        assert L.cram_get_knob(_lib.KNOB_DECODE_U) == 2
+        os.environ["CRAM_DECODE_U"] = "4"            # the environment is not re-read after the first query
+        assert L.cram_get_knob(_lib.KNOB_DECODE_U) == 2
+        with pytest.raises(RuntimeError):
+            _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, 5)
+    finally:
+        os.environ.pop("CRAM_DECODE_U", None)
+        _lib.set_knob(_lib.KNOB_DECODE_U, prev)
 
 
 def test_product_path_fails_loudly_without_library(tmp_path, monkeypatch):

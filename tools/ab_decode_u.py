@@ -1,4 +1,4 @@
-"""Same-process A/B of decode_kernel's keys-per-iteration U (CRAM_DECODE_U, read at every launch) at the decode
+"""Same-process A/B of decode_kernel's keys-per-iteration U (the library knob CRAM_KNOB_DECODE_U) at the decode
 leg's shape (B sequences of ragged length, Llama-3 GQA 4:1, credibility bias on half the heads).
 
     [AB_HEADS=Hq,Hkv,d] python tools/ab_decode_u.py [B] [S] [U list, e.g. 4,2,1]
@@ -10,7 +10,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from cram_amd import ops  # noqa: E402
+from cram_amd import _lib, ops  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
@@ -30,7 +30,7 @@ ref = None
 res = {}
 for rnd in range(5):
     for u in (sys.argv[3].split(",") if len(sys.argv) > 3 else ("4", "2", "1")):
-        os.environ["CRAM_DECODE_U"] = u
+        _lib.set_knob(_lib.KNOB_DECODE_U, int(u))
         run = lambda: ops.attn_decode(q, kc, vc, scale=d ** -0.5, seq_lens=lens, bias=bias, enable=enable, W=S,
                                       out=out)
         run()

@@ -1,5 +1,5 @@
-"""Same-process interleaved A/B of prefill-kernel variants (CRAM_PREFILL_VARIANT is read by the library at every
-launch): N rounds x variants x shapes, median ms per launch.  Usage: python tools/ab_prefill_inproc.py f0 f7 ..."""
+"""Same-process interleaved A/B of prefill-kernel variants (the library's CRAM_KNOB_PREFILL_VARIANT knob, -1 / 3 / 8):
+N rounds x variants x shapes, median ms per launch.  Usage: python tools/ab_prefill_inproc.py -1 3 8"""
 import os
 import statistics
 import sys
@@ -7,9 +7,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from cram_amd import ops  # noqa: E402
+from cram_amd import _lib, ops  # noqa: E402
 
-variants = sys.argv[1:] or ["0", "f7"]
+variants = sys.argv[1:] or ["-1", "8"]
 dev = torch.device("cuda:0")
 d = 128
 shapes = [(33, 962), (1, 8300)]
@@ -23,7 +23,7 @@ for B, T in shapes:
 res = {(vv, s): [] for vv in variants for s in shapes}
 for rnd in range(5):
     for vv in variants:
-        os.environ["CRAM_PREFILL_VARIANT"] = vv
+        _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, int(vv))
         for s in shapes:
             q, k, v, out = data[s]
             for _ in range(2):

@@ -1,6 +1,6 @@
 """IE noise of the GPU path vs the float32 truth, next to the reference's own bf16 error (per question).
 
-Run on the GPU box, once per kernel variant:  CRAM_PREFILL_VARIANT=3 python tools/ie_noise_probe.py
+Run on the GPU box, once per kernel variant:  python tools/ie_noise_probe.py (variant knob: CRAM_PREFILL_VARIANT, read once at start)
 """
 import gzip, json, os, sys
 import numpy as np
