@@ -109,13 +109,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
     ap.add_argument("--decode-batch", type=int, default=256)
-    ap.add_argument("--decode-tokens", type=int, default=16)
+    ap.add_argument("--decode-tokens", type=int, default=100, help="new tokens per question (re_weighting.py:127)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--scores", default="ideal", choices=["ideal", "gpt"],
                     help="decode scores: ideal [0.1,1,1,1,1] or the NQ GPT truthful scores (RAG_test.py:89-105)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefix-skip", action="store_true", help="recompute rows before the first biased key (A/B)")
-    ap.add_argument("--cpu-units", type=int, default=2)
+    ap.add_argument("--cpu-units", type=int, default=8, help="IE units of the CPU baseline sample (>= 1)")
     ap.add_argument("--blas", default="hipblaslt", choices=["hipblas", "hipblaslt"])
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPU) or gloo (rehearsal)")
     ap.add_argument("--model", default=None, choices=["llama3-8b", "qwen2-7b", "llama2-13b"],
@@ -165,52 +165,58 @@ def main():
     # ------------------------------------------------------------------ IE sweep (config 3)
     ie = None
     if args.config == 3:
-        n_q = (args.warmup + args.steps) * world
+        n_w, n_t = args.warmup * world, args.steps * world
         # weak scaling with equal per-GPU work at every N: questions are taken in order of closeness to the
-        # mean prompt length (characters of question + passages + wrong answer), step s on rank r gets the
-        # (s * N + r)-th, so the max-over-ranks step time does not grow with N from prompt-length spread alone
+        # mean prompt length (characters of question + passages + wrong answer); the warm-up and the timed set
+        # (steps x N questions) each go through the product's sharded sweep (cram_amd.dist.sweep_sharded: LPT of
+        # whole questions over the ranks by token count, one RCCL all-gather of the IE rows at the end)
         clen = [len(r["question"]) + sum(len(p) for p in r["ori_fake"] + r["reranked_dense_ctxs"])
                 + len(r["wrong_answer"]) for r in data]
         mean_c = sum(clen) / len(clen)
         pool = sorted(range(len(data)), key=lambda i: (abs(clen[i] - mean_c), i))
         work = []
-        for s in range(args.warmup + args.steps):
-            qi = pool[(s * world + rank) % len(pool)]
+        for s in range(n_w + n_t):
+            qi = pool[s % len(pool)]
             rec = data[qi]
             _, enc, w, _ = spans.encode(tok, name, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
                                         [0, 1, 1, 1, 1], rec["wrong_answer"])
             ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
             work.append((qi, enc["input_ids"][0].to(dev), w[0], ans.to(dev)))
         torch.cuda.synchronize()
-        for s in range(args.warmup):
-            qi, ids, w, ans = work[s]
-            sweep.ie_question(eng, ids, w, ans, skip_prefix=not args.no_prefix_skip)
-            torch.cuda.synchronize()
-            log(f"[rank {rank}] warmup step {s} done")
+        mine = []
+
+        def run_set(items, timed):
+            def fn(i, layers):
+                qi, ids, w, ans = items[i]
+                out = sweep.ie_question(eng, ids, w, ans, layers=layers, skip_prefix=not args.no_prefix_skip)
+                if timed:
+                    mine.append((ids.numel(), ans.numel(), w, layers))
+                log(f"[rank {rank}] {'step' if timed else 'warmup'} question {qi}: {len(layers)} layers enqueued "
+                    f"({time.perf_counter() - t_start:.1f}s)")
+                return out
+            return cdist.sweep_sharded(fn, len(items), [x[1].numel() for x in items], L, H, dev)
+
+        t_start = time.perf_counter()
+        if n_w:
+            run_set(work[:n_w], False)
+        torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         ops.TIMER.reset()
         ops.TIMER.enabled = True
         t_start = time.perf_counter()
-        flops = 0.0
-        timed = []
-        for s in range(args.steps):
-            qi, ids, w, ans = work[args.warmup + s]
-            timed.append(sweep.ie_question(eng, ids, w, ans, skip_prefix=not args.no_prefix_skip))
-            p0 = int((w.view(-1) != 1).nonzero()[0, 0]) if bool((w != 1).any()) else ids.numel()
-            p0 = 0 if args.no_prefix_skip else p0
-            flops += sweep.sweep_flops(spec, ids.numel(), ans.numel(), p0)
-            if rank == 0:
-                log(f"[rank 0] step {s} enqueued ({time.perf_counter() - t_start:.1f}s)")
-        local_ie = torch.stack(timed)
-        local_ids = torch.tensor([(args.warmup + s) * world + rank for s in range(args.steps)], dtype=torch.int64)
-        full = cdist.gather_rows(local_ie, local_ids, n_q)          # the sweep's RCCL all-gather
+        full = run_set(work[n_w:], True)                     # sweep + the RCCL all-gather of the IE grid
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t_start
         ops.TIMER.enabled = False
+        flops = 0.0
+        for T, n_ans, w, layers in mine:
+            p0 = int((w.view(-1) != 1).nonzero()[0, 0]) if bool((w != 1).any()) else T
+            p0 = 0 if args.no_prefix_skip else p0
+            flops += sweep.sweep_flops(spec, T, n_ans, p0, layers)
         ksum = ops.TIMER.summary()
         kt, kg = ksum.get("cram_prefill", None), ksum.get("gemm", None)
         el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -218,8 +224,8 @@ def main():
         if world > 1:
             el, fl = cdist.all_reduce_host(el, "max"), cdist.all_reduce_host(fl, "sum")
         elapsed, flops_all = float(el.item()), float(fl.item())
-        units = world * args.steps * L * H
-        assert torch.isfinite(full[args.warmup * world:]).all(), "non-finite IE"
+        units = n_t * L * H
+        assert tuple(full.shape) == (n_t, L, H) and torch.isfinite(full).all(), "non-finite or missing IE"
         ie = {"value": units / elapsed, "elapsed": elapsed, "flops": flops_all, "kt": kt, "kg": kg,
               "mean_T": sum(x[1].numel() for x in work) / len(work), "work": work}
         log(f"[rank {rank}] IE sweep: {units} units in {elapsed:.2f}s -> {ie['value']:.1f} heads/s")
@@ -295,12 +301,16 @@ def main():
         t0 = time.time()
         cpu_model = cpu_baseline.hf_model_from_engine(eng)
         qi, ids, w, ans = ie["work"][0]
-        units_s = [(0, 0), (L - 1, H - 1), (L // 2, 3), (1, 7)][:args.cpu_units]
+        units_s = cpu_baseline.sample_units(L, H, max(1, args.cpu_units))
         r = cpu_baseline.time_ie_units(cpu_model, ids.cpu(), w, ans.cpu(), units_s)
+        sp_ = r["spread"]
         cpu = {"value": r["units_per_s"], "unit": "heads/s", "cores": r["cores"], "kind": "port",
-               "sample": f"{r['units']} IE units (hooked full forward + full-vocab logits + .item(), "
-                         f"re_weighting.py:162-171) of NQ question {qi} at T'={ids.numel()}, after 1 un-hooked "
-                         f"forward; {r['seconds']:.1f}s; {result['dtype']} torch CPU; extrapolates linearly per unit"}
+               "sample": f"{r['units']} IE units {units_s} over {len(set(l for l, _ in units_s))} layers (hooked full "
+                         f"forward + full-vocab logits + .item(), re_weighting.py:162-171) of NQ question {qi} at "
+                         f"T'={ids.numel()}, after 1 un-hooked forward; {r['seconds']:.1f}s; {result['dtype']} torch "
+                         f"CPU; extrapolates linearly per unit",
+               "unit_seconds": {"min": round(sp_["min_s"], 3), "median": round(sp_["median_s"], 3),
+                                "max": round(sp_["max_s"], 3)}}
         del cpu_model
         log(f"[rank 0] cpu baseline {cpu['value']:.4f} heads/s on {cpu['cores']} cores ({time.time() - t0:.0f}s)")
 
@@ -343,7 +353,10 @@ def main():
                 "data": f"synthetic: random-init {name} weights; rebuilt NQ-1000 prompts via offline BPE tokenizer",
                 "config": {"workload": f"{name} Find_Best_Heads IE sweep, {L} layers x {H} heads per question, "
                                        "scores [0,1,1,1,1], 1 NQ question per GPU per step (config 3; decode = config 2)",
-                           "model": model, "questions_per_step": world, "question_order": "nearest the mean NQ prompt length first, dealt round-robin to ranks", "mean_prompt_tokens": round(ie["mean_T"], 1),
+                           "model": model, "questions_per_step": world,
+                           "question_order": "nearest the mean NQ prompt length first; steps x N questions dealt to "
+                                             "ranks by cram_amd.dist.plan (LPT on token counts)",
+                           "mean_prompt_tokens": round(ie["mean_T"], 1),
                            "parallelism": f"dp{world} question-sharded + RCCL all-gather of IE"},
                 "roofline": roof,
                 "dominant_kernel": dom,

@@ -1,17 +1,30 @@
 """Multi-GPU sharding of the IE sweep: one process per GPU, static work lists, one RCCL all-gather.
 
-The sweep units are independent given the prompt.  Questions are
-dealt to ranks by a static LPT (longest-processing-time-first) assignment on
-their token counts, so no data-path collective is needed; at the end one
-`all_gather_into_tensor` (backend "nccl" = RCCL over xGMI on MI355X, "gloo" in
-the CPU tests) assembles the fp32 IE grid [Nq, L, H] on every rank.  Decode is
-replica-only (question-sharded, no collective).
+The sweep units are independent given the prompt.  The work item is
+(question, set of layers): with at least as many questions as ranks, whole
+questions are dealt by a static LPT (longest-processing-time-first) assignment on
+their token counts (one baseline forward per question); with fewer questions than
+ranks — e.g. one question's cal_logits on 8 GPUs — every question's layers are
+dealt to all ranks in a snake order (layer l costs ~ L - l suffix layer-forwards),
+each rank running the question's baseline forward for its own layers.  No
+data-path collective is needed; at the end one `all_gather_into_tensor` (backend
+"nccl" = RCCL over xGMI on MI355X, "gloo" in the CPU tests) assembles the fp32 IE
+grid [Nq, L, H] on every rank.
+
+Checkpoint / resume (find_best_heads.py:30-40,53-58 resumes by skipping questions
+already on file): with `shard_dir`, every rank appends one JSON line per finished
+(question, layer) to its own file `rank{r}.jsonl` (append-only, fsync'd per work
+item); a restarted run — any world size — reads every shard file, skips the units
+already there and fills them from disk.  Decode is replica-only (question-sharded,
+no collective).
 """
 from __future__ import annotations
 
+import glob
 import heapq
+import json
 import os
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -89,11 +102,13 @@ def gather_rows(local: torch.Tensor, local_ids: torch.Tensor, n_total: int, grou
     kmax_t = torch.tensor([local.shape[0]], device=dev, dtype=torch.int64)
     dist.all_reduce(kmax_t, op=dist.ReduceOp.MAX, group=group)
     kmax = int(kmax_t.item())
-    row = int(torch.tensor(local.shape[1:]).prod().item()) if local.dim() > 1 else 1
+    row = 1
+    for s in local.shape[1:]:
+        row *= int(s)
     buf = torch.zeros((kmax, row + 1), dtype=torch.float64, device=dev)
     buf[:, 0] = -1
     buf[:local.shape[0], 0] = local_ids.to(dev, torch.float64)
-    buf[:local.shape[0], 1:] = local.reshape(local.shape[0], -1).double()
+    buf[:local.shape[0], 1:] = local.reshape(local.shape[0], row).double()   # a rank may hold no rows
     allb = torch.empty((world * kmax, row + 1), dtype=torch.float64, device=dev)
     dist.all_gather_into_tensor(allb, buf, group=group)
     keep = allb[:, 0] >= 0
@@ -103,12 +118,85 @@ def gather_rows(local: torch.Tensor, local_ids: torch.Tensor, n_total: int, grou
     return out.reshape((n_total,) + tuple(local.shape[1:])).to(device=home, dtype=local.dtype)
 
 
-def sweep_questions(fn, n_questions: int, costs: Sequence[float], row_shape: Tuple[int, ...], device,
-                    group=None) -> torch.Tensor:
-    """Run fn(i) -> IE row_shape for this rank's LPT share of questions and all-gather [Nq, *row_shape]."""
+WorkItem = Tuple[int, List[int]]          # (question index, layers)
+
+
+def plan(costs: Sequence[float], num_layers: int, world: int) -> List[List[WorkItem]]:
+    """Static per-rank work lists [(question, layers)] for the IE sweep (see the module docstring)."""
+    nq = len(costs)
+    if nq >= world:
+        return [[(i, list(range(num_layers))) for i in b] for b in lpt_shards(costs, world)]
+    snake = snake_layers(num_layers, world)
+    return [[(i, list(snake[r])) for i in range(nq)] if snake[r] else [] for r in range(world)]
+
+
+def read_shards(shard_dir: str, num_heads: int) -> Dict[Tuple[int, int], List[float]]:
+    """{(question, layer): IE row} from every rank's append-only file; a torn last line (a killed writer) is
+    ignored, a later line for the same unit wins."""
+    done: Dict[Tuple[int, int], List[float]] = {}
+    for fn in sorted(glob.glob(os.path.join(shard_dir, "rank*.jsonl"))):
+        with open(fn, encoding="utf-8") as f:
+            for line in f:
+                try:
+                    rec = json.loads(line)
+                except ValueError:
+                    continue
+                if isinstance(rec, dict) and len(rec.get("ie", ())) == num_heads:
+                    done[(int(rec["q"]), int(rec["layer"]))] = [float(x) for x in rec["ie"]]
+    return done
+
+
+class ShardWriter:
+    """Append-only per-rank checkpoint file: one line {"q", "layer", "ie"} per finished (question, layer)."""
+
+    def __init__(self, shard_dir: str, rank: int, qid: Optional[Sequence] = None):
+        os.makedirs(shard_dir, exist_ok=True)
+        self.path = os.path.join(shard_dir, f"rank{rank}.jsonl")
+        self.qid = qid
+
+    def write(self, q: int, layers: Sequence[int], ie_rows) -> None:
+        rows = ie_rows.tolist() if hasattr(ie_rows, "tolist") else ie_rows
+        lines = []
+        for l, row in zip(layers, rows):
+            rec = {"q": int(q), "layer": int(l), "ie": [float(x) for x in row]}
+            if self.qid is not None:
+                rec["id"] = self.qid[q]
+            lines.append(json.dumps(rec) + "\n")
+        with open(self.path, "a", encoding="utf-8") as f:
+            f.write("".join(lines))
+            f.flush()
+            os.fsync(f.fileno())
+
+
+def sweep_sharded(fn: Callable[[int, List[int]], torch.Tensor], n_questions: int, costs: Sequence[float],
+                  num_layers: int, num_heads: int, device, shard_dir: Optional[str] = None, group=None,
+                  qid: Optional[Sequence] = None, log: Optional[Callable[[str], None]] = None) -> torch.Tensor:
+    """IE [Nq, L, H] (fp32, on `device`, identical on every rank) of n_questions questions.
+
+    fn(i, layers) -> IE rows [len(layers), H] of question i (cram_amd.sweep.ie_question(..., layers=layers)).
+    Work is planned by `plan`; with shard_dir, finished units are checkpointed per work item and a restarted
+    run skips every unit already on disk.  The rows computed in this run travel in ONE all-gather."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    mine = lpt_shards(costs, world)[rank]
-    res = [fn(i).to(device, torch.float32) for i in mine]
-    local = torch.stack(res) if res else torch.zeros((0,) + tuple(row_shape), dtype=torch.float32, device=device)
-    return gather_rows(local, torch.tensor(mine, dtype=torch.int64), n_questions, group)
+    done = read_shards(shard_dir, num_heads) if shard_dir else {}
+    if shard_dir and world > 1:
+        dist.barrier(group)                   # every rank has read the same files before anyone appends
+    writer = ShardWriter(shard_dir, rank, qid) if shard_dir else None
+    rows, ids = [], []
+    for q, layers in plan(costs, num_layers, world)[rank]:
+        todo = [l for l in layers if (q, l) not in done]
+        if not todo:
+            continue
+        ie = fn(q, todo).to(device, torch.float32)
+        if writer is not None:
+            writer.write(q, todo, ie)
+        rows.append(ie)
+        ids.extend(q * num_layers + l for l in todo)
+        if log is not None:
+            log(f"[rank {rank}] question {q}: {len(todo)} layers")
+    local = torch.cat(rows) if rows else torch.zeros((0, num_heads), dtype=torch.float32, device=device)
+    out = gather_rows(local, torch.tensor(ids, dtype=torch.int64), n_questions * num_layers, group)
+    for (q, l), row in done.items():
+        if q < n_questions and l < num_layers:
+            out[q * num_layers + l] = torch.tensor(row, dtype=torch.float32, device=out.device)
+    return out.view(n_questions, num_layers, num_heads)

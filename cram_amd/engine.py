@@ -148,7 +148,7 @@ class CrAMEngine:
         self.dtype = embed.dtype
         self.scale = spec.head_dim ** -0.5
         if self.device.type == "cuda":
-            gemm_tune.ensure()          # pinned q/k/v and o_proj GEMM solutions (no-op on another BLAS build)
+            gemm_tune.ensure()          # pinned q/k/v and o_proj GEMM solutions, used inside gemm_tune.pinned()
 
     # ------------------------------------------------------------------ construction
     SUPPORTED = ("llama", "qwen2")
@@ -335,14 +335,18 @@ class CrAMEngine:
     @torch.no_grad()
     def generate(self, prompts: Sequence[torch.Tensor], weights16: Sequence[torch.Tensor], layers_to_heads: dict,
                  max_new_tokens: int = 100, eos_ids: Sequence[int] = (), bad_token_ids: Sequence[int] = (),
-                 use_graph: bool = True, stop_on_eos: bool = True) -> List[List[int]]:
+                 use_graph: bool = True, stop_on_eos: bool = True,
+                 repetition_penalty: float = 1.0) -> List[List[int]]:
         """Greedy decode of several prompts at once (per-row lengths, per-row credibility bias).
 
         Returns the generated ids of every prompt, truncated after its first EOS
         (tokens generated after EOS are never observed, so per-row results equal
-        one-at-a-time generation as in re_weighting.py:127-132).
+        one-at-a-time generation as in re_weighting.py:127-132).  repetition_penalty != 1 applies transformers'
+        RepetitionPenaltyLogitsProcessor (the checkpoint's generation_config, e.g. Qwen chat models ship 1.05)
+        over each row's prompt and generated ids.
         """
-        sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids)
+        sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids,
+                             repetition_penalty)
         sess.prefill()
         steps = max_new_tokens - 1
         if use_graph and steps > 0:
@@ -370,7 +374,8 @@ class CrAMEngine:
 class DecodeSession:
     """Static-shape state of one batched greedy decode (KV cache, bias, token buffers)."""
 
-    def __init__(self, eng: CrAMEngine, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids=()):
+    def __init__(self, eng: CrAMEngine, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids=(),
+                 repetition_penalty: float = 1.0):
         sp = eng.spec
         self.eng = eng
         self.B = len(prompts)
@@ -391,6 +396,16 @@ class DecodeSession:
         self.out = torch.zeros((self.B, max_new_tokens), dtype=torch.long, device=dev)
         self.t = torch.zeros((), dtype=torch.long, device=dev)                    # next output column
         self.bad = torch.tensor(list(bad_token_ids), dtype=torch.long, device=dev) if bad_token_ids else None
+        # repetition penalty (transformers RepetitionPenaltyLogitsProcessor): the set of ids each row has seen so
+        # far (prompt + generated) as a [B, V] mask, updated inside the (graph-captured) step
+        self.penalty = float(repetition_penalty)
+        self.seen = None
+        if self.penalty != 1.0:
+            if self.penalty <= 0:
+                raise ValueError("repetition_penalty must be > 0")
+            self.seen = torch.zeros((self.B, eng.lm_head.shape[0]), dtype=torch.bool, device=dev)
+            for b, p in enumerate(self.prompts):
+                self.seen[b, p] = True
         splits = max(1, min(16, math.ceil(512 / max(1, self.B * sp.num_kv_heads))))
         self.splits = max(1, min(splits, self.S_max // 256))
         self.ws = (torch.empty(ops.decode_workspace_bytes(self.B, sp.num_heads, sp.head_dim, self.splits),
@@ -399,10 +414,20 @@ class DecodeSession:
         self.rows = torch.arange(self.B, device=dev)
         self.cos, self.sin = eng.rope_tables(self.S_max)
 
-    def _pick(self, logits: torch.Tensor) -> torch.Tensor:
+    def _pick(self, logits: torch.Tensor, rows: Optional[slice] = None) -> torch.Tensor:
+        """Greedy choice as transformers' generate makes it: fp32 logits, the repetition penalty (score / p where
+        positive, score * p where negative, on the row's seen ids), bad words to -inf, argmax."""
+        if self.seen is not None:
+            x = logits.float()
+            seen = self.seen if rows is None else self.seen[rows]
+            logits = torch.where(seen, torch.where(x < 0, x * self.penalty, x / self.penalty), x)
         if self.bad is not None:
             logits = logits.index_fill(-1, self.bad, float("-inf"))
-        return torch.argmax(logits, dim=-1)
+        nxt = torch.argmax(logits, dim=-1)
+        if self.seen is not None:
+            r = self.rows if rows is None else self.rows[rows]
+            self.seen[r, nxt] = True
+        return nxt
 
     def prefill(self, max_rows: int = PREFILL_CHUNK_ROWS):
         """All prompts in packed varlen passes of at most ``max_rows`` tokens each (GEMM M = the chunk's token
@@ -412,13 +437,14 @@ class DecodeSession:
         the same blocks across chunks and calls (one 231k-row pass made it map fresh multi-GB segments, a ~1 s
         host stall per call)."""
         b0 = 0
-        while b0 < self.B:
-            b1, rows = b0, 0
-            while b1 < self.B and (b1 == b0 or rows + self.lens[b1] <= max_rows):
-                rows += self.lens[b1]
-                b1 += 1
-            self._prefill_chunk(b0, b1)
-            b0 = b1
+        with gemm_tune.pinned():
+            while b0 < self.B:
+                b1, rows = b0, 0
+                while b1 < self.B and (b1 == b0 or rows + self.lens[b1] <= max_rows):
+                    rows += self.lens[b1]
+                    b1 += 1
+                self._prefill_chunk(b0, b1)
+                b0 = b1
         self.out[:, 0] = self.tokens
         self.t.fill_(1)
 
@@ -466,7 +492,7 @@ class DecodeSession:
             m = eng.mlp(x2, lw)
         last = cu[1:].long() - 1
         _, hn = ops.rmsnorm(m[last], eng.norm, sp.eps, residual=h[last])
-        self.tokens[b0:b1] = self._pick(ops.linear(hn, eng.lm_head))
+        self.tokens[b0:b1] = self._pick(ops.linear(hn, eng.lm_head), slice(b0, b1))
 
     def _step_body(self):
         eng, sp = self.eng, self.eng.spec

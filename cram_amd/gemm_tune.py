@@ -9,9 +9,14 @@ back with tuning off.  Shapes without a line (decode steps, other models) run th
 
 The solution ids belong to one hipBLASLt / rocBLAS build: the file carries the validators of the build they
 were tuned on (`data/gemm_solutions.json`), and nothing is pinned when the running build differs.
+
+Scope: TunableOp is a process-wide switch, so it is only turned on inside `pinned()` blocks — the engine's
+sweep and packed prefill — and restored to the caller's state on exit; other GEMMs of the process (the
+transformers model of the drop-in path, user code) keep torch's default selection and TunableOp settings.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 import tempfile
@@ -57,13 +62,36 @@ def install(m_values: Iterable[int], dtype: str = "BFloat16", path: str = SOLUTI
     fd, fn = tempfile.mkstemp(prefix="cram_gemm_", suffix=".csv")
     with os.fdopen(fd, "w") as f:
         f.write("\n".join(lines) + "\n")
-    torch.cuda.tunable.enable(True)
-    torch.cuda.tunable.tuning_enable(False)
-    torch.cuda.tunable.record_untuned_enable(False)
-    ok = torch.cuda.tunable.read_file(fn)
-    os.unlink(fn)
+    tun = torch.cuda.tunable
+    prev = (tun.is_enabled(), tun.tuning_is_enabled())
+    tun.enable(True)
+    tun.tuning_enable(False)
+    try:
+        ok = tun.read_file(fn)
+    finally:
+        tun.enable(prev[0])
+        tun.tuning_enable(prev[1])
+        os.unlink(fn)
     _installed = fn if ok else None
     return bool(ok)
+
+
+@contextlib.contextmanager
+def pinned():
+    """Use the pinned solutions for the GEMMs issued inside the block (TunableOp on, tuning off), then restore
+    the process's previous TunableOp state.  A no-op when nothing was pinned (other build, no GPU, A/B off)."""
+    if not _tried:
+        yield
+        return
+    tun = torch.cuda.tunable
+    prev = (tun.is_enabled(), tun.tuning_is_enabled())
+    tun.enable(True)
+    tun.tuning_enable(False)
+    try:
+        yield
+    finally:
+        tun.enable(prev[0])
+        tun.tuning_enable(prev[1])
 
 
 def sweep_rows(lo: int = 8192, hi: int = 65536, step: int = 256) -> Tuple[int, ...]:
@@ -72,7 +100,8 @@ def sweep_rows(lo: int = 8192, hi: int = 65536, step: int = 256) -> Tuple[int, .
 
 
 def ensure() -> bool:
-    """Install the pins once per process (CrAMEngine does this on a GPU); False when the build differs."""
+    """Load the pins once per process (CrAMEngine does this on a GPU; they act inside `pinned()` only); False
+    when the build differs."""
     global _tried
     if _tried is None:
         off = os.environ.get("CRAM_GEMM_PIN", "1") == "0"              # A/B switch: default heuristic everywhere
@@ -81,4 +110,5 @@ def ensure() -> bool:
 
 
 def uninstall() -> None:
-    torch.cuda.tunable.enable(False)
+    global _tried
+    _tried = False

@@ -91,6 +91,31 @@ def casual_tracing_per_head(data: list, model, output_file: str, contexts_type=(
     return done
 
 
+def casual_tracing_per_head_sharded(data: list, model, output_file: str, shard_dir: str,
+                                    contexts_type=("ori_fake", "reranked_dense"), topk: int = 4, group=None) -> list:
+    """casual_tracing_per_head (find_best_heads.py:13-58) over one process per GPU: the (question, layer) units of
+    all questions are sharded over the ranks (cram_amd.dist.plan), every rank checkpoints its finished units in
+    shard_dir/rank{r}.jsonl (a restarted run of any world size skips them), one all-gather assembles [Nq, L, H]
+    and rank 0 writes heads_scores.json in the reference's format.  `model` is a Find_Best_Heads."""
+    import torch.distributed as tdist
+    qs, ps, ss, ws = [], [], [], []
+    for sample in data:
+        ctx, sc = sweep_contexts(sample, contexts_type, topk)
+        qs.append(sample["question"])
+        ps.append(ctx)
+        ss.append(sc)
+        ws.append(sample.get("wrong answer", sample.get("wrong_answer")))
+    ie = model.cal_logits_batch(qs, ps, ss, ws, shard_dir=shard_dir, group=group)
+    res = ie.double().cpu().numpy().tolist()
+    if not tdist.is_initialized() or tdist.get_rank(group) == 0:
+        os.makedirs(os.path.dirname(os.path.abspath(output_file)), exist_ok=True)
+        tmp = output_file + ".tmp"
+        with open(tmp, "w", encoding="utf-8") as f:
+            json.dump(res, f, ensure_ascii=False, indent=4)
+        os.replace(tmp, output_file)
+    return res
+
+
 def position_contexts(sample: dict, position: int, contexts_type=("ori_fake", "reranked_dense"), topk: int = 4):
     """find_best_heads.py:83-99: the retrieved passages before `position`, then the fake passage(s), then the rest.
 

@@ -142,6 +142,22 @@ class Re_Weighting_Strategy:
         lp = torch.log_softmax(logits.float(), dim=-1)
         return lp.gather(1, ids[0, T - n:].view(n, 1)).view(n)
 
+    def _greedy_processors(self) -> float:
+        """The logits processors model.generate(do_sample=False) would apply from the checkpoint's
+        generation_config (re_weighting.py:127-132 passes none of its own besides bad_words_ids / eos): the
+        repetition penalty is returned for the engine; any other score-changing processor raises rather than
+        silently diverging from the reference's greedy ids."""
+        gc = self.model.generation_config
+        unsupported = {"no_repeat_ngram_size": 0, "encoder_repetition_penalty": 1.0, "min_length": 0,
+                       "min_new_tokens": None, "suppress_tokens": None, "begin_suppress_tokens": None,
+                       "forced_bos_token_id": None, "forced_eos_token_id": None, "sequence_bias": None,
+                       "exponential_decay_length_penalty": None, "renormalize_logits": False}
+        for k, default in unsupported.items():
+            v = getattr(gc, k, default)
+            if v not in (default, None, 0, False, [], {}):
+                raise NotImplementedError(f"generation_config.{k}={v!r} is not implemented by the batched engine")
+        return float(getattr(gc, "repetition_penalty", None) or 1.0)
+
     @torch.no_grad()
     def run_RAG_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
                       max_new_tokens: int = 100, use_graph: bool = True) -> List[tuple]:
@@ -150,13 +166,14 @@ class Re_Weighting_Strategy:
         prompts = [ids.to(self.device) for ids, _, _ in encs]
         ws = [w for _, w, _ in encs]
         kw = self._generate_kwargs()
+        penalty = self._greedy_processors()
         eos = kw.get("eos_token_id", self.model.generation_config.eos_token_id)
         eos = [eos] if isinstance(eos, int) else list(eos or [])
         bad = [b[0] for b in self.bad_words_ids if len(b) == 1]
         if len(bad) != len(self.bad_words_ids):
             raise NotImplementedError("multi-token bad_words_ids are not supported by the batched engine")
         gens = self.engine.generate(prompts, ws, self.layers_to_be_modified, max_new_tokens=max_new_tokens,
-                                    eos_ids=eos, bad_token_ids=bad, use_graph=use_graph)
+                                    eos_ids=eos, bad_token_ids=bad, use_graph=use_graph, repetition_penalty=penalty)
         res = []
         for ids, g in zip(prompts, gens):
             full = torch.cat([ids.cpu(), torch.tensor(g, dtype=ids.dtype)])
@@ -184,26 +201,28 @@ class Find_Best_Heads(Re_Weighting_Strategy):
 
     @torch.no_grad()
     def cal_logits_tensor(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
-                          wrong_answer: str = "my name is", round_logits: bool = False) -> torch.Tensor:
-        """IE [L, H] fp32 on the device (no host sync)."""
+                          wrong_answer: str = "my name is", round_logits: bool = False,
+                          layers: Optional[List[int]] = None) -> torch.Tensor:
+        """IE [L, H] (or [len(layers), H] for a subset of layers) fp32 on the device (no host sync)."""
         ans = self.answer_ids(wrong_answer)
         model_inputs, w = self.decode_with_special_attention(question=question, paras=paras, scores=scores,
                                                              answer=wrong_answer)
-        L, H = self.model_num_hidden_layers, self.model_num_attention_heads
+        layers = list(range(self.model_num_hidden_layers)) if layers is None else list(layers)
+        H = self.model_num_attention_heads
         if ans.numel() == 0:   # the reference sums an empty selection: IE == 0 everywhere
-            return torch.zeros((L, H), dtype=torch.float32, device=self.device)
+            return torch.zeros((len(layers), H), dtype=torch.float32, device=self.device)
         if not CrAMEngine.supports(self.model):
-            return self._ie_per_head(model_inputs["input_ids"], w, ans, round_logits)
-        return _sweep.ie_question(self.engine, model_inputs["input_ids"][0], w[0].cpu(), ans,
+            return self._ie_per_head(model_inputs["input_ids"], w, ans, round_logits, layers)
+        return _sweep.ie_question(self.engine, model_inputs["input_ids"][0], w[0].cpu(), ans, layers=layers,
                                   round_logits=round_logits)
 
     @torch.no_grad()
     def _ie_per_head(self, ids: torch.Tensor, w16: torch.Tensor, ans: torch.Tensor,
-                     round_logits: bool) -> torch.Tensor:
+                     round_logits: bool, layers: List[int]) -> torch.Tensor:
         """The reference algorithm itself (re_weighting.py:157-175: one un-hooked forward, then one forward per
         (layer, head) with only that head re-weighted) on the transformers model with the cram_hip kernels, for
         architectures the batched engine does not implement (GPT-2).  Answer logits in fp32 like the sweep."""
-        L, H = self.model_num_hidden_layers, self.model_num_attention_heads
+        H = self.model_num_attention_heads
         n = int(ans.numel())
         ans_d = ans.to(self.device, torch.int32)
         w_lm = self.model.get_output_embeddings().weight
@@ -214,10 +233,10 @@ class Find_Best_Heads(Re_Weighting_Strategy):
             return self._answer_logits(hid, w_lm, ans_d, round_logits).sum()
 
         ori = total(None)
-        out = torch.empty((L, H), dtype=torch.float32, device=self.device)
-        for l in range(L):
+        out = torch.empty((len(layers), H), dtype=torch.float32, device=self.device)
+        for i, l in enumerate(layers):
             for h in range(H):
-                out[l, h] = ori - total(self._bias(w16, {l: [h]}))
+                out[i, h] = ori - total(self._bias(w16, {l: [h]}))
         return out
 
     @staticmethod
@@ -228,13 +247,21 @@ class Find_Best_Heads(Re_Weighting_Strategy):
 
     @torch.no_grad()
     def cal_logits_batch(self, questions: List[str], paras_list: List[list], scores_list: List[list],
-                         wrong_answers: List[str], round_logits: bool = False) -> torch.Tensor:
-        """IE of many questions as one device tensor [Nq, L, H] fp32 (the sweep's batched form)."""
-        out = torch.empty((len(questions), self.model_num_hidden_layers, self.model_num_attention_heads),
-                          dtype=torch.float32, device=self.device)
-        for i, (q, p, s, a) in enumerate(zip(questions, paras_list, scores_list, wrong_answers)):
-            out[i] = self.cal_logits_tensor(q, p, s, "", a, round_logits)
-        return out
+                         wrong_answers: List[str], round_logits: bool = False, shard_dir: Optional[str] = None,
+                         group=None) -> torch.Tensor:
+        """IE of many questions as one device tensor [Nq, L, H] fp32 (the sweep's batched form).
+
+        Under torch.distributed (one process per GPU) the (question, layer) units are sharded over the ranks
+        (cram_amd.dist.plan: whole questions by LPT, or one question's layers snake-split when there are fewer
+        questions than ranks) and assembled on every rank by one all-gather; with shard_dir every rank
+        checkpoints its finished units and a restarted run resumes from them (cram_amd.dist.sweep_sharded)."""
+        from . import dist as _dist
+        costs = [float(len(q) + sum(len(x) for x in p) + len(a))
+                 for q, p, a in zip(questions, paras_list, wrong_answers)]
+        fn = lambda i, layers: self.cal_logits_tensor(questions[i], paras_list[i], scores_list[i], "",
+                                                      wrong_answers[i], round_logits, layers=layers)
+        return _dist.sweep_sharded(fn, len(questions), costs, self.model_num_hidden_layers,
+                                   self.model_num_attention_heads, self.device, shard_dir=shard_dir, group=group)
 
     def cal_logits(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
                    wrong_answer: str = "my name is") -> list:

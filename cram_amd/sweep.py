@@ -31,7 +31,7 @@ from typing import Optional
 
 import torch
 
-from . import ops
+from . import gemm_tune, ops
 from .bias import CredibilityBias
 from .engine import CrAMEngine, padded_rows
 
@@ -138,6 +138,11 @@ def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answ
     ids [T'] (prompt + answer), weight16 fp16 [T'] (sweep scores), answer_ids [n]
     (standalone tokenisation, first id dropped: re_weighting.py:155).
     """
+    with gemm_tune.pinned():
+        return _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_prefix)
+
+
+def _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_prefix):
     sp = eng.spec
     dev = eng.device
     ids = ids.to(dev).view(-1)
@@ -157,8 +162,9 @@ def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answ
     return out
 
 
-def sweep_flops(spec, T: int, n_ans: int, p0: int = 0) -> float:
-    """Algorithmic GEMM+attention flops of ie_question (for roofline accounting); p0 = skipped prefix rows."""
+def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None) -> float:
+    """Algorithmic GEMM+attention flops of ie_question(layers=...) (for roofline accounting): one baseline
+    forward plus the suffix work of every swept layer; p0 = skipped prefix rows."""
     L, H, d, D = spec.num_layers, spec.num_heads, spec.head_dim, spec.hidden
 
     def attn(tq, s):   # tq queries at positions s-tq .. s-1, causal
@@ -173,7 +179,7 @@ def sweep_flops(spec, T: int, n_ans: int, p0: int = 0) -> float:
     f = 0.0
     # baseline: L-1 full layers + last layer (qkv over T, rest over n)
     f += (L - 1) * (lay(T) + attn(T, T)) + qkv_frac * lay(T) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T)
-    for l in range(L):
+    for l in (range(L) if layers is None else layers):
         last = l == L - 1
         rows = n_ans if last else Ts
         f += attn(rows, T)                                              # all-heads biased attention

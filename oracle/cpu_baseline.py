@@ -75,8 +75,9 @@ def time_ie_units(model, ids: torch.Tensor, w16: torch.Tensor, answer_ids: torch
     am = torch.ones_like(ids)
     ori = hook_ref.answer_logit_sum(model(input_ids=ids, attention_mask=am).logits, answer_ids)
     t0 = time.perf_counter()
-    vals = []
+    vals, per = [], []
     for (l, h) in units:
+        t1 = time.perf_counter()
         hs = hook_ref.register_hooks(model, {l: [h]}, lw)
         try:
             cur = hook_ref.answer_logit_sum(model(input_ids=ids, attention_mask=am).logits, answer_ids)
@@ -84,6 +85,19 @@ def time_ie_units(model, ids: torch.Tensor, w16: torch.Tensor, answer_ids: torch
             for x in hs:
                 x.remove()
         vals.append((ori - cur).item())
+        per.append(time.perf_counter() - t1)
     dt = time.perf_counter() - t0
+    srt = sorted(per)
     return {"units": len(units), "seconds": dt, "units_per_s": len(units) / dt, "cores": cores(),
-            "ie": vals}
+            "ie": vals, "unit_seconds": per,
+            "spread": {"min_s": srt[0], "median_s": srt[len(srt) // 2], "max_s": srt[-1]}}
+
+
+def sample_units(num_layers: int, num_heads: int, n: int):
+    """n (layer, head) units spread over the layers (first, last, middle, quarters, ...) and heads."""
+    fr = [0.0, 1.0, 0.5, 0.25, 0.75, 0.125, 0.625, 0.375, 0.875]
+    out = []
+    for i in range(n):
+        l = round(fr[i % len(fr)] * (num_layers - 1)) if i < len(fr) else (i * 7) % num_layers
+        out.append((int(l), int((i * 11 + 3) % num_heads)))
+    return out

@@ -1,7 +1,13 @@
-"""Multi-process (gloo, world_size 2) tests of the IE-sweep sharding and the final all-gather.
+"""Multi-process (gloo) tests of the IE-sweep sharding, checkpoint / resume and the final all-gather.
 
-The GPU path runs the same code with backend "nccl" (RCCL over xGMI); here the
-kernels are the CPU stand-ins of tests/cpu_ops.py.
+The GPU path runs the same code with backend "nccl" (RCCL over xGMI); here the kernels are the CPU stand-ins of
+tests/cpu_ops.py.  Every sharded result must equal the single-process sweep bit for bit:
+  * world 2, 3 questions: whole questions dealt by LPT;
+  * world 4 and 8, 3 questions (fewer questions than ranks): every question's layers snake-split over the ranks
+    (cal_logits of one question on several GPUs);
+  * resume after a kill: a world-4 run whose rank 1 dies after its first work item (the spawner then tears the
+    others down mid-flight), restarted at world 2 from the per-rank shard files — the restart computes only the
+    units missing on disk (find_best_heads.py:30-40,53-58 resume semantics, at (question, layer) granularity).
 """
 import gzip
 import json
@@ -14,6 +20,9 @@ import torch
 import torch.multiprocessing as mp
 
 from cram_amd import dist as cdist
+
+KIND = "llama3"          # tiny Llama-3: 4 layers x 4 heads (GQA 2:1)
+NQ = 3
 
 
 def test_lpt_and_snake():
@@ -29,10 +38,32 @@ def test_lpt_and_snake():
     assert cdist.lpt_shards([1.0], 4)[1:] == [[], [], []]
 
 
+def test_plan_covers_every_unit_once():
+    for nq, L, world in [(1, 32, 8), (3, 32, 8), (8, 32, 8), (1000, 32, 8), (5, 4, 2), (3, 4, 8), (1, 28, 3)]:
+        p = cdist.plan([100 + (i * 37) % 11 for i in range(nq)], L, world)
+        assert len(p) == world
+        units = [(q, l) for items in p for q, ls in items for l in ls]
+        assert sorted(units) == [(q, l) for q in range(nq) for l in range(L)]
+    # one question on 8 ranks: every rank gets layers, snake-balanced (cost of layer l ~ L - l)
+    p = cdist.plan([900.0], 32, 8)
+    loads = [sum(32 - l for _, ls in items for l in ls) for items in p]
+    assert min(loads) > 0 and max(loads) - min(loads) <= 8
+
+
 def test_gather_rows_single_process():
     local = torch.arange(6.0).view(2, 3)
     out = cdist.gather_rows(local, torch.tensor([3, 0]), 4)
     assert torch.equal(out[3], local[0]) and torch.equal(out[0], local[1]) and out[1].abs().sum() == 0
+
+
+def test_shard_files_tolerate_a_torn_line(tmp_path):
+    w = cdist.ShardWriter(str(tmp_path), 0)
+    w.write(2, [0, 3], torch.tensor([[1.5, -2.0], [0.25, 3.0]]))
+    with open(tmp_path / "rank0.jsonl", "a") as f:
+        f.write('{"q": 2, "layer": 1, "ie": [0.1')       # a writer killed mid-line
+    cdist.ShardWriter(str(tmp_path), 1).write(1, [1], [[7.0, 8.0]])
+    done = cdist.read_shards(str(tmp_path), 2)
+    assert done == {(2, 0): [1.5, -2.0], (2, 3): [0.25, 3.0], (1, 1): [7.0, 8.0]}
 
 
 def _free_port():
@@ -41,61 +72,103 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, root, out_path):
+def _inputs(path):
+    from transformers import AutoTokenizer
+    from cram_amd import spans
+    from tests import tiny_models as tm
+    tok = AutoTokenizer.from_pretrained(path)
+    with gzip.open(os.path.join(tm.REPO, "data", "nq_1000.json.gz"), "rt") as f:
+        nq = json.load(f)[:NQ]
+    out = []
+    for rec in nq:
+        _, enc, wt, _ = spans.encode(tok, path, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
+                                     [0, 1, 1, 1, 1], rec["wrong_answer"])
+        ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
+        out.append((enc["input_ids"][0], wt[0], ans))
+    return out
+
+
+def _worker(rank, world, port, root, out_path, shard_dir, die_after):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
-    torch.set_num_threads(2)
-    from transformers import AutoModelForCausalLM, AutoTokenizer
-    from cram_amd import spans, sweep
+    torch.set_num_threads(1)
+    from transformers import AutoModelForCausalLM
+    from cram_amd import sweep
     from cram_amd.engine import CrAMEngine
     from tests import cpu_ops
     from tests import tiny_models as tm
     r, w, _ = cdist.init("gloo")
     assert (r, w) == (rank, world)
-    path = os.path.join(root, "Qwen2-tiny")
-    tok = AutoTokenizer.from_pretrained(path)
+    path = os.path.join(root, tm.DIR_NAME[KIND])
     eng = CrAMEngine.from_hf(AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval())
-    with gzip.open(os.path.join(tm.REPO, "data", "nq_1000.json.gz"), "rt") as f:
-        nq = json.load(f)[:3]
-    inputs = []
-    for rec in nq:
-        _, enc, wt, _ = spans.encode(tok, path, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
-                                     [0, 1, 1, 1, 1], rec["wrong_answer"])
-        ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
-        inputs.append((enc["input_ids"][0], wt[0], ans))
+    inputs = _inputs(path)
+    calls = []
+
+    def fn(i, layers):
+        if die_after is not None and rank == die_after[0] and len(calls) == die_after[1]:
+            os._exit(3)                                      # killed between two work items
+        calls.append((i, list(layers)))
+        return sweep.ie_question(eng, *inputs[i], layers=layers)
+
     with cpu_ops.patched_ops():
-        full = cdist.sweep_questions(lambda i: sweep.ie_question(eng, *inputs[i]), len(inputs),
-                                     [x[0].numel() for x in inputs], (eng.spec.num_layers, eng.spec.num_heads),
-                                     torch.device("cpu"))
+        full = cdist.sweep_sharded(fn, len(inputs), [x[0].numel() for x in inputs], eng.spec.num_layers,
+                                   eng.spec.num_heads, torch.device("cpu"), shard_dir=shard_dir)
+    with open(f"{out_path}.calls{rank}.json", "w") as f:
+        json.dump(calls, f)
     if rank == 0:
         np.save(out_path, full.numpy())
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
 
-def test_two_rank_sweep_matches_single_process(tmp_path):
-    from tests import tiny_models as tm
-    root = str(tmp_path)
-    tm.save_model("qwen2", root)
-    out = str(tmp_path / "ie2.npy")
-    mp.spawn(_worker, args=(2, _free_port(), root, out), nprocs=2, join=True)
-    two = np.load(out)
-    # single-process reference of the same three questions
-    from transformers import AutoModelForCausalLM, AutoTokenizer
-    from cram_amd import spans, sweep
+@pytest.fixture(scope="module")
+def single(tmp_path_factory):
+    """Single-process sweep of the same questions (the bar for every sharded run)."""
+    from transformers import AutoModelForCausalLM
+    from cram_amd import sweep
     from cram_amd.engine import CrAMEngine
     from tests import cpu_ops
-    path = os.path.join(root, "Qwen2-tiny")
-    tok = AutoTokenizer.from_pretrained(path)
+    from tests import tiny_models as tm
+    root = str(tmp_path_factory.mktemp("dist"))
+    path = tm.save_model(KIND, root)
     eng = CrAMEngine.from_hf(AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval())
-    with gzip.open(os.path.join(tm.REPO, "data", "nq_1000.json.gz"), "rt") as f:
-        nq = json.load(f)[:3]
-    one = []
     with cpu_ops.patched_ops():
-        for rec in nq:
-            _, enc, wt, _ = spans.encode(tok, path, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
-                                         [0, 1, 1, 1, 1], rec["wrong_answer"])
-            ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
-            one.append(sweep.ie_question(eng, enc["input_ids"][0], wt[0], ans).numpy())
-    np.testing.assert_array_equal(two, np.stack(one))
-    assert np.abs(two).sum() > 0
+        one = np.stack([sweep.ie_question(eng, *x).numpy() for x in _inputs(path)])
+    assert np.abs(one).sum() > 0
+    return root, one
+
+
+def _spawn(root, world, out, shard_dir=None, die_after=None):
+    mp.spawn(_worker, args=(world, _free_port(), root, out, shard_dir, die_after), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_sweep_matches_single_process(tmp_path, single, world):
+    root, one = single
+    out = str(tmp_path / f"ie{world}.npy")
+    _spawn(root, world, out)
+    np.testing.assert_array_equal(np.load(out), one)
+    calls = [json.load(open(f"{out}.calls{r}.json")) for r in range(world)]
+    units = sorted((q, l) for c in calls for q, ls in c for l in ls)
+    assert units == [(q, l) for q in range(NQ) for l in range(one.shape[1])]      # every unit exactly once
+    if world > NQ:                                                                 # layer split of each question
+        assert all(len(ls) < one.shape[1] for c in calls for _, ls in c)
+
+
+def test_resume_after_kill(tmp_path, single):
+    root, one = single
+    shards = str(tmp_path / "shards")
+    out = str(tmp_path / "ie.npy")
+    with pytest.raises(Exception):
+        _spawn(root, 4, out, shard_dir=shards, die_after=(1, 1))
+    done = cdist.read_shards(shards, one.shape[2])
+    assert 0 < len(done) < NQ * one.shape[1]
+    for (q, l), row in done.items():                       # what reached the disk is final
+        np.testing.assert_array_equal(np.asarray(row, dtype=np.float32), one[q, l])
+    _spawn(root, 2, out, shard_dir=shards)
+    np.testing.assert_array_equal(np.load(out), one)
+    calls = [json.load(open(f"{out}.calls{r}.json")) for r in range(2)]
+    redone = {(q, l) for c in calls for q, ls in c for l in ls}
+    assert not redone & set(done), "a unit on disk was recomputed"
+    assert len(redone) + len(done) == NQ * one.shape[1]
+    assert len(cdist.read_shards(shards, one.shape[2])) == NQ * one.shape[1]

@@ -174,6 +174,44 @@ def test_engine_batched_decode_matches_dropin(paths, nq, gpu_device):
                 break
 
 
+def test_engine_repetition_penalty_matches_dropin(paths, nq, gpu_device):
+    """Qwen chat checkpoints ship generation_config.repetition_penalty = 1.05, which model.generate applies in
+    greedy decoding: run_RAG_batch (engine, graph-replayed) must apply it too.  The tiny Qwen2's config is set to
+    1.05 and to 1.5 (a penalty that changes ids within 24 tokens); ids equal the drop-in's model.generate up to
+    the first near-tie (top-2 gap < 0.05 after the penalty)."""
+    heads = {0: [0], 2: [1]}
+    obj = _drop_in(paths, "qwen2", heads, gpu_device)
+    qs = [nq[i] for i in range(3)]
+    args = ([q["question"] for q in qs], [q["ori_fake"] + q["reranked_dense_ctxs"] for q in qs],
+            [[0.1, 1, 1, 1, 1]] * 3)
+    from cram_amd import attention as A
+    gc = obj.model.generation_config
+    old = gc.repetition_penalty
+    try:
+        for pen in (1.05, 1.5):
+            gc.repetition_penalty = pen
+            assert obj._greedy_processors() == pen
+            batched = obj.run_RAG_batch(*args, max_new_tokens=24, use_graph=True)
+            assert batched == obj.run_RAG_batch(*args, max_new_tokens=24, use_graph=False)
+            for i in range(3):
+                enc, w = obj.decode_with_special_attention(question=args[0][i], paras=args[1][i], scores=args[2][i])
+                cb = obj._bias(w, heads)
+                with A.reweighting(obj.model, cb), torch.no_grad():
+                    out = obj.model.generate(**enc, do_sample=False, max_new_tokens=24, output_scores=True,
+                                             return_dict_in_generate=True)
+                ref = out.sequences[0, enc["input_ids"].shape[1]:].tolist()
+                got = obj.engine.generate([enc["input_ids"][0]], [w.cpu()], heads, max_new_tokens=24,
+                                          eos_ids=[gc.eos_token_id] if isinstance(gc.eos_token_id, int)
+                                          else list(gc.eos_token_id or []), repetition_penalty=pen)[0]
+                gaps = _gaps(out.scores)
+                for t in range(min(len(ref), len(got))):
+                    if ref[t] != got[t]:
+                        assert min(gaps[:t + 1]) < 0.05, (pen, i, t, gaps[t])
+                        break
+    finally:
+        gc.repetition_penalty = old
+
+
 def test_batched_sweep_equals_unbatched_on_gpu(fbh, nq):
     from cram_amd import sweep
     from cram_amd.bias import CredibilityBias

@@ -220,6 +220,52 @@ def test_engine_batched_generate_matches_single(tiny, nq):
     assert one[1] == ref
 
 
+@pytest.mark.parametrize("kind", ["qwen2", "llama3"])
+def test_engine_repetition_penalty_matches_generate(tiny, nq, kind):
+    """Batched decode with the checkpoint's repetition penalty (Qwen chat generation_config ships 1.05; a strong
+    1.5 here so it changes the ids) == transformers' greedy generate with the same penalty and the hook."""
+    path, tok, model = tiny[kind]
+    eng = CrAMEngine.from_hf(model)
+    prompts, ws = [], []
+    for i, L in ((3, 150), (4, 190)):
+        ids, w = _question(tok, path, nq[i], answer=False)
+        prompts.append(ids[0, :L])
+        ws.append(w[:, :L])
+    heads = {0: [0], 1: [1]}
+    with cpu_ops.patched_ops():
+        pen = eng.generate(prompts, ws, heads, max_new_tokens=12, use_graph=False, repetition_penalty=1.5)
+        plain = eng.generate(prompts, ws, heads, max_new_tokens=12, use_graph=False)
+    assert pen != plain                                   # the penalty is in effect
+    for p, w, got in zip(prompts, ws, pen):
+        hs = hook_ref.register_hooks(model, heads, hook_ref.log_weight(w))
+        try:
+            with torch.no_grad():
+                ref = model.generate(input_ids=p[None], attention_mask=torch.ones_like(p[None]), do_sample=False,
+                                     max_new_tokens=12, repetition_penalty=1.5)[0, p.numel():].tolist()
+        finally:
+            for h in hs:
+                h.remove()
+        assert got == ref
+
+
+def test_greedy_processors_guard(tiny):
+    """run_RAG_batch takes the repetition penalty from generation_config and refuses processors it lacks."""
+    from cram_amd.re_weighting import Re_Weighting_Strategy
+    path, tok, model = tiny["qwen2"]
+    obj = Re_Weighting_Strategy.__new__(Re_Weighting_Strategy)
+    obj.model = model
+    gc = model.generation_config
+    old = (gc.repetition_penalty, gc.no_repeat_ngram_size)
+    try:
+        gc.repetition_penalty = 1.05
+        assert obj._greedy_processors() == 1.05
+        gc.no_repeat_ngram_size = 3
+        with pytest.raises(NotImplementedError):
+            obj._greedy_processors()
+    finally:
+        gc.repetition_penalty, gc.no_repeat_ngram_size = old
+
+
 def test_sweep_flops_accounting():
     from cram_amd.engine import ModelSpec
     sp = ModelSpec.llama3_8b()

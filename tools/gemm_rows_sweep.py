@@ -18,6 +18,8 @@ from cram_amd import gemm_tune  # noqa: E402
 lo, hi, step, rounds = (int(a) for a in (sys.argv[1:5] if len(sys.argv) >= 5 else (16384, 40960, 256, 5)))
 dev = torch.device("cuda:0")
 pinned = gemm_tune.install(gemm_tune.sweep_rows())
+torch.cuda.tunable.enable(True)              # pins act while TunableOp is on (gemm_tune.pinned)
+torch.cuda.tunable.tuning_enable(False)
 shapes = [(4096, 6144), (4096, 4096), (4096, 28672), (14336, 4096)]
 W = [(K, (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)) for K, N in shapes]
 X = {K: torch.randn(hi, K, device=dev).to(torch.bfloat16) for K in (4096, 14336)}

@@ -17,6 +17,8 @@ dev = torch.device("cuda:0")
 Ms = [int(a) for a in sys.argv[1:]] or [8192, 16384, 23040, 26112, 29184, 32768]
 shapes = [(4096, 6144), (4096, 4096), (4096, 28672), (14336, 4096)]
 print("pinned:", gemm_tune.install(gemm_tune.sweep_rows()), flush=True)
+torch.cuda.tunable.enable(True)              # pins act while TunableOp is on (gemm_tune.pinned)
+torch.cuda.tunable.tuning_enable(False)
 W = [(K, N, (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)) for K, N in shapes]
 X = {M: {K: torch.randn(M, K, device=dev).to(torch.bfloat16) for K in (4096, 14336)} for M in Ms}
 
