@@ -424,9 +424,8 @@ class DecodeSession:
         if self.bad is not None:
             logits = logits.index_fill(-1, self.bad, float("-inf"))
         nxt = torch.argmax(logits, dim=-1)
-        if self.seen is not None:
-            r = self.rows if rows is None else self.rows[rows]
-            self.seen[r, nxt] = True
+        if self.seen is not None:             # scatter of a scalar: no host tensor, capturable in the step graph
+            (self.seen if rows is None else self.seen[rows]).scatter_(1, nxt[:, None], True)
         return nxt
 
     def prefill(self, max_rows: int = PREFILL_CHUNK_ROWS):

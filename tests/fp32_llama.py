@@ -106,3 +106,60 @@ class Fp32Llama:
                 h = self.layer(h, l2, cos, sin, mask if l2 == l else causal.expand(self.sp.num_heads, T, T))
             out.append(float(ori - self.answer_sum(self.rms(h, self.norm), ans)))
         return out
+
+    @torch.no_grad()
+    def ie_grid(self, ids, bias, ans, layers=None):
+        """IE [len(layers), H] float64 of every (layer, head) unit, computed per layer as a batch of H hooked
+        variants (variant h: head h of layer l re-weighted; layers above l plain causal).  Mathematically the
+        same units as ie_units (one hooked forward per unit); only the fp32 GEMM shapes differ."""
+        sp = self.sp
+        T = ids.numel()
+        H = sp.num_heads
+        dev = self.norm.device
+        cos, sin = self.rope(T, dev)
+        hs, hf = self.baseline(ids)
+        ori = self.answer_sum(hf, ans)
+        causal = self.causal(T, dev)
+        hooked = causal.clone()
+        W = bias.numel()
+        allowed = causal[:, :W] == 0
+        hooked[:, :W] = torch.where(allowed, bias[None, :].expand(T, W), causal[:, :W])   # replace, :57-59
+        n = ans.numel()
+        w_ans = self.lm_head[ans.long()].float()
+        layers = range(sp.num_layers) if layers is None else layers
+        out = torch.empty((len(layers), H), dtype=torch.float64)
+        for i, l in enumerate(layers):
+            mask = causal.repeat(H, H, 1, 1)                          # [variant, head, T, T]
+            idx = torch.arange(H, device=dev)
+            mask[idx, idx] = hooked
+            h = hs[l].expand(H, T, sp.hidden).contiguous()
+            for l2 in range(l, sp.num_layers):
+                h = self.layer_batch(h, l2, cos, sin, mask if l2 == l else None)
+            hn = self.rms(h[:, -n:], self.norm)                       # [H, n, D]
+            cur = (hn * w_ans[None]).sum((1, 2))
+            out[i] = (ori - cur).double().cpu()
+        return out
+
+    def layer_batch(self, h, l, cos, sin, mask):
+        """layer() over a batch [B, T, D]; mask [B, Hq, T, T] additive, or None for plain causal."""
+        sp, w = self.sp, self.layers[l]
+        B, T, _ = h.shape
+        x = self.rms(h, w["ln1"])
+        y = x @ w["wqkv"].t()
+        if w["bqkv"] is not None:
+            y = y + w["bqkv"]
+        q = y[..., :sp.q_size].view(B, T, sp.num_heads, sp.head_dim).transpose(1, 2)
+        k = y[..., sp.q_size:sp.q_size + sp.kv_size].view(B, T, sp.num_kv_heads, sp.head_dim).transpose(1, 2)
+        v = y[..., sp.q_size + sp.kv_size:].view(B, T, sp.num_kv_heads, sp.head_dim).transpose(1, 2)
+        q, k = self.rot(q, cos, sin), self.rot(k, cos, sin)
+        g = sp.num_heads // sp.num_kv_heads
+        k, v = k.repeat_interleave(g, 1), v.repeat_interleave(g, 1)
+        if mask is None:
+            a = F.scaled_dot_product_attention(q, k, v, is_causal=True)
+        else:
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+        h = h + a.transpose(1, 2).reshape(B, T, sp.q_size) @ w["wo"].t()
+        x2 = self.rms(h, w["ln2"])
+        gu = x2 @ w["wgu"].t()
+        act = F.silu(gu[..., :sp.intermediate]) * gu[..., sp.intermediate:]
+        return h + act @ w["wd"].t()

@@ -266,6 +266,25 @@ def test_greedy_processors_guard(tiny):
         gc.repetition_penalty, gc.no_repeat_ngram_size = old
 
 
+def test_fp32_truth_batched_grid_equals_per_unit(tiny, nq):
+    """tests/fp32_llama.py: the per-layer batched float32 truth (used at the Llama-3-8B shape) equals one hooked
+    float32 forward per unit up to float32 rounding."""
+    from tests.fp32_llama import Fp32Llama
+    path, tok, model = tiny["llama3"]
+    eng = CrAMEngine.from_hf(model)
+    ids, w = _question(tok, path, nq[5], answer=True)
+    ids = ids[0, :180]
+    w = w[0, :180]
+    ans = ids[-3:]
+    f32 = Fp32Llama(eng)
+    bias = torch.log(w.float())
+    units = [(l, h) for l in range(eng.spec.num_layers) for h in range(eng.spec.num_heads)]
+    per = torch.tensor(f32.ie_units(ids, bias, ans, units), dtype=torch.float64).view(eng.spec.num_layers, -1)
+    grid = f32.ie_grid(ids, bias, ans)
+    assert per.abs().max() > 1e-3
+    assert (grid - per).abs().max() < 1e-4 * max(1.0, per.abs().max().item())
+
+
 def test_sweep_flops_accounting():
     from cram_amd.engine import ModelSpec
     sp = ModelSpec.llama3_8b()
