@@ -521,12 +521,15 @@ class DecodeSession:
         s = torch.cuda.Stream(self.eng.device)
         s.wait_stream(torch.cuda.current_stream(self.eng.device))
         # warm the allocator / kernels on a side stream, then restore the state it advanced
-        snap = (self.tokens.clone(), self.pos.clone(), self.seq_lens.clone(), self.t.clone(), self.out.clone())
+        snap = (self.tokens.clone(), self.pos.clone(), self.seq_lens.clone(), self.t.clone(), self.out.clone(),
+                None if self.seen is None else self.seen.clone())
         with torch.cuda.stream(s):
             self._step_body()
         torch.cuda.current_stream(self.eng.device).wait_stream(s)
         self.tokens.copy_(snap[0]); self.pos.copy_(snap[1]); self.seq_lens.copy_(snap[2])
         self.t.copy_(snap[3]); self.out.copy_(snap[4])
+        if self.seen is not None:
+            self.seen.copy_(snap[5])
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._step_body()
