@@ -61,6 +61,26 @@ __device__ __forceinline__ f32x16 mfma32x16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ f32x4 mfma16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x32(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// max / sum over lanes l, l^16, l^32, l^48 (the four 16-lane rows): one permlane16 and one permlane32 swap
+__device__ __forceinline__ float quad_max16(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+__device__ __forceinline__ float quad_sum16(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(t[0]) + __uint_as_float(t[1]);
+}
+
 // value from lane l^32 combined with own value (lane halves exchanged by one permlane32 swap)
 __device__ __forceinline__ float half_max(float x) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -686,6 +706,219 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
       static_cast<T*>(p.o)[b * p.o_sb + hq * p.o_sh + dd] = (T)(L > 0.f ? O / L : 0.f);
     } else {
       const int64_t slot = ((int64_t)(b * p.Hq + hq) * nsplit + split);
+      p.ws_o[slot * D + dd] = O;
+      if (dd == 0) { p.ws_ml[slot * 2 + 0] = M; p.ws_ml[slot * 2 + 1] = L; }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// decode on the matrix cores (GQA groups of 4..16 query heads, d = 128)
+// --------------------------------------------------------------------------------------------
+// All G query heads of one kv head against 32-key blocks, per wave, with v_mfma_f32_16x16x32:
+//   S^T[16 keys][16 q]  = K[16 keys][d] . Q^T[d][16 q]   (A = K rows straight from HBM into VGPRs: lane l loads
+//                                                          16 B of key row l&15; B = Q^T held for the whole loop)
+//   O^T[16 d][16 q]    += V^T[16 d][32 keys] . P^T[32 keys][16 q]
+// Lane l owns query head q = l&15 and keys 4(l>>4)+i (+16) of a block, which is exactly the B-operand slot
+// order of the PV product (slots 0-3 = keys 4g..4g+3, 4-7 = keys 16+4g..16+4g+3), so P goes from the score
+// registers to the operand by 4 conversions; V^T comes from a per-wave LDS image of the block's V rows
+// (register-staged, 288-B rows: the ds_read_b64_tr_b16 of 8 rows x 16 columns hit 64 distinct banks).
+// The waves of a workgroup take alternate key blocks and share nothing until the final combine, so the loop has
+// no barrier; K/V of the next block are loaded while the current one is computed.  Query heads >= G are zero
+// columns.  The VALU kernel spends ~G x 26 instructions per key and lane on the dot products, reductions and
+// online softmax: at G = 7 (Qwen2) that body read 2.9 TB/s; here the dot products run on the matrix cores.
+template <typename T, int G>
+__global__ __launch_bounds__(256, 2) void decode_mfma_kernel(DecodeParams p) {
+  constexpr int D = 128;
+  constexpr int VSTR = D * 2 + 32;          // V image row stride (bytes)
+  constexpr int KB = 32;                    // keys per block
+  constexpr int VIMG = KB * VSTR;           // 9216 B per wave
+  using V8 = typename Vec<T>::x8;
+  static_assert(G <= 16, "one 16-column MFMA tile of query heads");
+  __shared__ __attribute__((aligned(16))) char smem[4 * VIMG];
+
+  const int hkv = blockIdx.x, b = blockIdx.y, split = blockIdx.z, nsplit = gridDim.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int qi = lane & 15, grp = lane >> 4;
+
+  const int S_b = p.seq_lens ? p.seq_lens[b] : p.S;
+  const int chunk = (((S_b + nsplit - 1) / nsplit) + 63) & ~63;
+  const int k_begin = split * chunk;
+  const int k_end = min(S_b, k_begin + chunk);
+  const int nblk = k_end > k_begin ? (k_end - k_begin + KB - 1) / KB : 0;
+
+  // Q^T as the B operand: lane (q, g) holds Q[q][32c + 8g .. +7] for the four 32-d chunks c; q >= G -> 0
+  const int hq = hkv * G + qi;
+  V8 qf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (qi < G) {
+      qf[c] = *reinterpret_cast<const V8*>(static_cast<const T*>(p.q) + b * p.q_sb + hq * p.q_sh + 32 * c + 8 * grp);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[c][j] = (T)0.f;
+    }
+  }
+  const bool en = qi < G && p.bias != nullptr && p.enable != nullptr && p.enable[b * p.en_sb + hq] != 0;
+  const bool en_any = __builtin_amdgcn_ballot_w64(en) != 0;
+
+  // K / V rows through buffer descriptors bounded at k_end: rows past it read as zeros (no stale cache rows)
+  const T* kbase = static_cast<const T*>(p.k) + b * p.k_sb + hkv * p.k_sh;
+  const T* vbase = static_cast<const T*>(p.v) + b * p.v_sb + hkv * p.v_sh;
+  const int rows = max(k_end, 1);
+  const auto ksrd = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, (short)0, (int)((rows - 1) * p.k_st * 2 + D * 2),
+                                                      0x00020000);
+  const auto vsrd = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, (short)0, (int)((rows - 1) * p.v_st * 2 + D * 2),
+                                                      0x00020000);
+  const float* brow = p.bias ? p.bias + b * p.bias_sb : nullptr;
+  const auto bsrd = __builtin_amdgcn_make_buffer_rsrc((void*)brow, (short)0, en_any ? p.W * 4 : 0, 0x00020000);
+
+  // per-lane constant offsets
+  uint32_t koff[2][4];   // K: row (16 hh + q), bytes 64 c + 16 g
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) koff[hh][c] = (uint32_t)((16 * hh + qi) * p.k_st * 2 + 64 * c + 16 * grp);
+  const uint32_t vrow_off = (uint32_t)(grp * p.v_st * 2 + 16 * qi);   // V: rows 4 i + g, 16-B piece q
+  char* vimg = smem + wave * VIMG;
+  // ds_read_b64_tr_b16 base: lane 4 r + c4 of its 16-lane group supplies row 4 g + r, columns 4 c4 .. +3
+  const uint32_t tr_base = (uint32_t)(uintptr_t)(lds_void*)vimg + (uint32_t)((4 * grp + (qi >> 2)) * VSTR + (qi & 3) * 8);
+
+  using BV = __attribute__((ext_vector_type(4))) unsigned;
+  BV kn[2][4], vn[8];
+  f32x4 bn[2];
+  auto load_block = [&](int blk) {
+    const int key0 = k_begin + blk * KB;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        kn[hh][c] = __builtin_amdgcn_raw_buffer_load_b128(ksrd, (int)(koff[hh][c] + key0 * p.k_st * 2), 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      vn[i] = __builtin_amdgcn_raw_buffer_load_b128(vsrd, (int)(vrow_off + (key0 + 4 * i) * p.v_st * 2), 0, 0);
+    if (en_any) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const BV r = __builtin_amdgcn_raw_buffer_load_b128(bsrd, (key0 + 16 * hh + 4 * grp) * 4, 0, 0);
+        bn[hh] = __builtin_bit_cast(f32x4, r);
+      }
+    }
+  };
+
+  float m = kNegInf, l = 0.f;
+  f32x4 oacc[8];
+#pragma unroll
+  for (int db = 0; db < 8; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int blk = wave;
+  if (blk < nblk) load_block(blk);
+  for (; blk < nblk; blk += 4) {
+    const int key0 = k_begin + blk * KB;
+    BV kc[2][4];
+    f32x4 bc[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bc[hh] = bn[hh];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kc[hh][c] = kn[hh][c];
+    }
+    // V rows of this block into the wave's LDS image (in-order LDS: the previous block's tr-reads are done)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<BV*>(vimg + (4 * i + grp) * VSTR + 16 * qi) = vn[i];
+    if (blk + 4 < nblk) load_block(blk + 4);
+
+    // S^T = K . Q^T for the two 16-key halves
+    f32x4 sc[2];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc = mfma16x32(__builtin_bit_cast(V8, kc[hh][c]), qf[c], acc);
+      sc[hh] = acc;
+    }
+    // scale, credibility bias, length mask (log2 units); block max over this q's 32 keys (4 lanes x 8)
+    float mx = kNegInf;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float s = sc[hh][i] * p.scale_log2;
+        if (en) s = __builtin_fmaf(bc[hh][i], kLog2e, s);
+        s = (key0 + 16 * hh + 4 * grp + i < k_end) ? s : kNegInf;
+        sc[hh][i] = s;
+        mx = fmaxf(mx, s);
+      }
+    mx = quad_max16(mx);
+    const float mnew = fmaxf(m, mx);
+    const float muse = (mnew == kNegInf) ? 0.f : mnew;
+    const float alpha = fast_exp2(m - muse);
+    float rs = 0.f;
+    V8 pb;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pe = fast_exp2(sc[hh][i] - muse);
+        rs += pe;
+        pb[4 * hh + i] = (T)pe;
+      }
+    l = l * alpha + rs;
+    m = mnew;
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+      for (int db = 0; db < 8; ++db) oacc[db] *= alpha;
+    }
+    // O^T += V^T . P^T: per 16-d block two transposed reads (keys 4g..4g+3 and 16+4g..16+4g+3)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the V image writes above have landed
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      i16x4 r0, r1;
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r0) : "v"(tr_base), "i"(db * 32));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r1) : "v"(tr_base), "i"(16 * VSTR + db * 32));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const V8 va = __builtin_bit_cast(V8, __builtin_shufflevector(r0, r1, 0, 1, 2, 3, 4, 5, 6, 7));
+      oacc[db] = mfma16x32(va, pb, oacc[db]);
+    }
+  }
+
+  // row sums: the 4 lanes of a query head hold disjoint keys under the same running max
+  l = quad_sum16(l);
+  __syncthreads();                                   // every wave is done with its V image: reuse the LDS
+  float* red_o = reinterpret_cast<float*>(smem);     // [4 waves][G][D]
+  float* red_ml = red_o + 4 * G * D;                 // [4 waves][G][2]
+  if (qi < G) {
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red_o[(wave * G + qi) * D + 16 * db + 4 * grp + i] = oacc[db][i];
+    if (grp == 0) {
+      red_ml[(wave * G + qi) * 2 + 0] = m;
+      red_ml[(wave * G + qi) * 2 + 1] = l;
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < G * D; idx += 256) {
+    const int g = idx / D, dd = idx % D;
+    float M = kNegInf;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, red_ml[(w * G + g) * 2]);
+    const float Muse = (M == kNegInf) ? 0.f : M;
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float a = fast_exp2(red_ml[(w * G + g) * 2] - Muse);
+      L += red_ml[(w * G + g) * 2 + 1] * a;
+      O += red_o[(w * G + g) * D + dd] * a;
+    }
+    const int h = hkv * G + g;
+    if (nsplit == 1) {
+      static_cast<T*>(p.o)[b * p.o_sb + h * p.o_sh + dd] = (T)(L > 0.f ? O / L : 0.f);
+    } else {
+      const int64_t slot = ((int64_t)(b * p.Hq + h) * nsplit + split);
       p.ws_o[slot * D + dd] = O;
       if (dd == 0) { p.ws_ml[slot * 2 + 0] = M; p.ws_ml[slot * 2 + 1] = L; }
     }

@@ -83,10 +83,12 @@ def main():
         ours.append(sweep.ie_question(eng, ids, w16, ans).double().cpu().numpy())
         torch.cuda.synchronize()
         t1 = time.time()
+        log(f"question {qi}: sweep done ({t1 - t0:.1f}s)")
         lw = hook_ref.log_weight(w16.view(1, -1)).to(dev)
         ref.append(hook_ref.ie_grid(hf, ids[None], lw, ans, upcast_logits=True))
         torch.cuda.synchronize()
         t2 = time.time()
+        log(f"question {qi}: reference hook grid done ({t2 - t1:.1f}s)")
         truth.append(f32.ie_grid(ids, torch.log(w16.to(dev).float()), ans).numpy())
         torch.cuda.synchronize()
         t3 = time.time()
