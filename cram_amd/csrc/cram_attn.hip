@@ -980,6 +980,8 @@ inline void knobs_init() {
   g_knob[CRAM_KNOB_PREFILL_VARIANT] = (e && (e[0] == '3' || e[0] == '8')) ? e[0] - '0' : -1;
   const char* eu = getenv("CRAM_DECODE_U");
   g_knob[CRAM_KNOB_DECODE_U] = (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1;
+  const char* em = getenv("CRAM_DECODE_MFMA");
+  g_knob[CRAM_KNOB_DECODE_MFMA] = (em && (em[0] == '0' || em[0] == '1')) ? em[0] - '0' : -1;
   g_knob_init = true;
 }
 inline int knob(int k) {
@@ -1023,6 +1025,19 @@ int dispatch_prefill(PrefillParams& p, int d, int dtype, hipStream_t stream) {
 
 template <typename T, int D, int G>
 int launch_decode_g(DecodeParams& p, int nsplit, hipStream_t stream) {
+  // GQA groups of >= 4 heads at d = 128 run on the matrix cores unless the knob says otherwise
+  const int km = knob(CRAM_KNOB_DECODE_MFMA);
+  if constexpr (D == 128 && G >= 4) {
+    if (km != 0) {
+      hipLaunchKernelGGL((decode_mfma_kernel<T, G>), dim3(p.Hkv, p.B, nsplit), dim3(256), 0, stream, p);
+      if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
+      if (nsplit > 1) {
+        hipLaunchKernelGGL((decode_combine_kernel<T, D>), dim3(p.Hq, p.B), dim3(D), 0, stream, p, nsplit);
+        if (hipGetLastError() != hipSuccess) return CRAM_ERR_LAUNCH;
+      }
+      return CRAM_OK;
+    }
+  }
   // keys per lane group per iteration: with >= 1024 workgroups (e.g. the batch-256 decode leg) occupancy is what
   // keeps K/V reads in flight: U = 1 (114 VGPRs, four waves per SIMD) read 4.73 TB/s, U = 2 (149, three) 4.56,
   // U = 4 (205, two) 4.12 (tools/ab_decode_u.py, B = 256); at 512 workgroups U = 4's deeper per-wave prefetch
@@ -1084,6 +1099,7 @@ int cram_set_knob(int which, int value) {
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;
+  if (which == CRAM_KNOB_DECODE_MFMA && value != -1 && value != 0 && value != 1) return CRAM_ERR_INVALID_ARG;
   g_knob[which] = value;
   return CRAM_OK;
 }

@@ -60,15 +60,18 @@ int cram_abi_version(void);
 
 /*
  * Process-wide kernel-selection knobs (A/B runs and tests; the product default is automatic = -1).
- * The initial values are read once from the environment (CRAM_PREFILL_VARIANT, CRAM_DECODE_U) at the first
- * query; no launch reads the environment.  Not synchronised: set knobs before launching from other threads.
+ * The initial values are read once from the environment (CRAM_PREFILL_VARIANT, CRAM_DECODE_U, CRAM_DECODE_MFMA) at
+ * the first query; no launch reads the environment.  Not synchronised: set knobs before launching from other
+ * threads.
  *   CRAM_KNOB_PREFILL_VARIANT  -1 / 0 = 64-key tiles, 4 waves (default); 3 = 32-key tiles; 8 = 8-wave workgroups
- *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration
+ *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
+ *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
  * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob returns the value.
  */
 #define CRAM_KNOB_PREFILL_VARIANT 0
 #define CRAM_KNOB_DECODE_U 1
-#define CRAM_KNOB_COUNT 2
+#define CRAM_KNOB_DECODE_MFMA 2
+#define CRAM_KNOB_COUNT 3
 int cram_set_knob(int which, int value);
 int cram_get_knob(int which);
 

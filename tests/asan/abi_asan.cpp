@@ -104,6 +104,9 @@ static void validation_paths() {
   EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, 2) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_U) == 2);
   EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, -1) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_U) == -1);
   EXPECT(cram_get_knob(7) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, 2) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, 0) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_MFMA) == 0);
+  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, -1) == CRAM_OK);
 }
 
 static uint16_t f16_bits(float x) {

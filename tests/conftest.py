@@ -34,11 +34,14 @@ def prefill_variant(request):
     _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, prev)
 
 
-@pytest.fixture(params=["auto", "u1", "u2"])
+@pytest.fixture(params=["auto", "valu_u1", "valu_u2", "valu_u4"])
 def decode_variant(request):
-    """Run a decode test on every decode_kernel instantiation: the size-picked keys-per-iteration U (1 for grids of
-    >= 1024 workgroups, else 4) and the forced U = 1 / 2 (knob CRAM_KNOB_DECODE_U)."""
+    """Run a decode test on every decode body: the automatic choice (matrix-core kernel for GQA groups of >= 4 heads
+    at d = 128, else the VALU kernel with its size-picked U) and the VALU kernel forced with U = 1 / 2 / 4 keys per
+    lane group (knobs CRAM_KNOB_DECODE_MFMA = 0, CRAM_KNOB_DECODE_U)."""
     from cram_amd import _lib
-    prev = _lib.set_knob(_lib.KNOB_DECODE_U, -1 if request.param == "auto" else int(request.param[1]))
+    mf, u = (-1, -1) if request.param == "auto" else (0, int(request.param[-1]))
+    prev = (_lib.set_knob(_lib.KNOB_DECODE_MFMA, mf), _lib.set_knob(_lib.KNOB_DECODE_U, u))
     yield request.param
-    _lib.set_knob(_lib.KNOB_DECODE_U, prev)
+    _lib.set_knob(_lib.KNOB_DECODE_MFMA, prev[0])
+    _lib.set_knob(_lib.KNOB_DECODE_U, prev[1])
