@@ -65,6 +65,8 @@ SIGNATURES = {
         c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_int, c_int, c_void_p,
     ]),
     "cram_silu_mul": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
+    "cram_gemm": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int,
+                          c_void_p]),
     "cram_passage_weights": (c_int, [c_int] + [c_void_p] * 9),
 }
 

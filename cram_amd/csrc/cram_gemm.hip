@@ -1,0 +1,328 @@
+// cram_gemm.hip — the IE sweep's projection GEMMs on the gfx950 matrix cores, with the MLP activation fused.
+//
+// out[m, n] = sum_k y[m, k] * x[n, k]: activations y [M, K] and nn.Linear weights x [N, K], both K-contiguous
+// (F.linear's layout, the only one the sweep uses).  The reference runs these as transformers' nn.Linear calls
+// inside every hooked forward (/root/reference/utils/re_weighting.py:158, :170); here they are the 87 % of the
+// head-batched sweep step.
+//
+// Epilogues
+//   CRAM_GEMM_STORE     out = rnd(acc)
+//   CRAM_GEMM_SILU_MUL  the LlamaMLP activation on a gate/up weight whose rows are interleaved in blocks of 32
+//                       (rows 64j .. 64j+31 = gate rows 32j .. 32j+31, rows 64j+32 .. 64j+63 = the matching up
+//                       rows): out[m, f] = rnd(rnd(silu(rnd(g))) * rnd(u)) — transformers' act_fn(gate_proj(x)) *
+//                       up_proj(x) on the rounded projections, i.e. cram_silu_mul's arithmetic — so the [M, 2F]
+//                       gate/up intermediate never reaches HBM (written once and read back once per layer before).
+//
+// Structure (one 512-thread workgroup per CU, 256 x 256 output tile, K in 64-deep tiles):
+//   * 8 waves as 2 (weight rows, "x") x 4 (activation rows, "y"); a wave owns 128 n x 64 m = 8 x 4 tiles of
+//     v_mfma_f32_16x16x32 (x fragments are the A operand, so a lane's accumulator holds 4 consecutive n of one m).
+//   * Both operands reach LDS by LDS-DMA (buffer_load_dwordx4 ... lds), two 64 KiB stages.  Rows are 128 B with
+//     16-byte chunk c of row r stored at slot c ^ ((r >> 1) & 7): every ds_read_b128 lane group of a fragment
+//     read hits 16 distinct slots (conflict-free).  LDS-DMA writes lane-linearly, so the permutation is applied
+//     to the per-lane SOURCE address and undone on the read.
+//   * A K-tile is 4 phases (quadrants of the wave's tile: 64 n x 32 m x K 64 = 16 MFMAs), each phase a memory
+//     interval (fragment reads + one quarter of the staging) and an MFMA interval separated by s_barrier.  Waves
+//     4-7 run one interval behind waves 0-3 (one extra barrier up front), so on every SIMD one wave issues MFMAs
+//     while its partner issues its reads: the matrix pipe is fed from two waves in turn.
+//   * Staging per K-tile in four 16 KiB units (x rows 0-63|128-191, y rows 32-blocks 0,2,4,6, y 1,3,5,7, x
+//     64-127|192-255), each issued into the other stage as soon as every wave has consumed the unit it replaces;
+//     one counted `s_waitcnt vmcnt(6)` per K-tile retires the next tile while two units of the tile after it stay
+//     in flight across the barriers (never vmcnt(0) in the steady loop; raw s_barrier, no __syncthreads fence).
+// Requirements (checked by the C-ABI): N % 256 == 0, K % 64 == 0, 16-byte aligned rows; any M >= 1 (rows past M
+// read as zeros through the buffer descriptor's range and are not stored).
+// Measured at the sweep shape (M = 29,184, bf16 random operands, same-process medians, tools/gemm_probe.py): q/k/v
+// 1.00-1.03x hipBLASLt, o_proj 0.97x, gate/up 0.92x, down 0.93x; gate/up + SiLU-mul fused 1.00-1.01x hipBLASLt +
+// cram_silu_mul.  The vendor kernel keeps its matrix pipe busy 82 % of the time (4 waves of 128 x 128) against 70 %
+// here.  Measured dead ends: one wave per SIMD at 128 x 128 (accumulators pinned in AGPRs by inline
+// asm) with LDS-DMA staging 0.81x, with register staging 0.72x, with no staging at all 1.08x (the staging
+// instructions in the MFMA wave's own stream are the whole gap); 8 waves software-pipelined with one barrier per
+// K-tile 0.85x; a two-phase ping-pong (4 barriers per K-tile) 0.89x.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "../../include/cram_attn.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <typename T> struct GVec;
+template <> struct GVec<__bf16> { typedef bf16x8 x8; typedef bf16x4 x4; };
+template <> struct GVec<_Float16> { typedef f16x8 x8; typedef f16x4 x4; };
+
+__device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f32x4& c, __bf16) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f32x4& c, _Float16) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                0);
+}
+
+// round to the element type and back (the model-dtype rounding transformers applies between ops)
+template <typename T>
+__device__ __forceinline__ float rnd(float x) { return (float)(T)x; }
+
+constexpr int BM = 256;            // activation rows per tile (y)
+constexpr int BN = 256;            // weight rows per tile (x)
+constexpr int BK = 64;             // K per tile: 128-byte LDS rows
+constexpr int ROWB = BK * 2;       // bytes per LDS row
+constexpr int IMG = 256 * ROWB;    // 32 KiB: one operand's image of one K-tile
+constexpr int STAGE = 2 * IMG;     // x image | y image
+constexpr int LDS_BYTES = 2 * STAGE;
+
+struct GemmParams {
+  const void* x; int64_t ldx;      // weights [N, K]
+  const void* y; int64_t ldy;      // activations [M, K]
+  void* out; int64_t ldo;          // [M, N] (store) or [M, N / 2] (silu-mul)
+  int M, N, K;
+  int ntm, ntn, nblocks;
+};
+
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Tile order: bijective XCD remap (each XCD a contiguous run of work ids), then groups of 8 weight tiles with the
+// activation tiles innermost, so the 32 workgroups an XCD runs at once share 4 y and 8 x panels.
+__device__ __forceinline__ void tile_of(const GemmParams& p, int bid, int& tm, int& tn) {
+  const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int GN = 8;
+  const int grp = wid / (GN * p.ntm);
+  const int gw = min(GN, p.ntn - grp * GN);
+  const int rem = wid - grp * GN * p.ntm;
+  tn = grp * GN + rem % gw;
+  tm = rem / gw;
+}
+
+// Epilogue shared by the kernels: lane (j, g) holds acc[a][b][i] = out[m + 16 b][n + 16 a + i] with
+// m = tile row + j, n = tile column + 4 g (NA x-tiles of 16 weight rows, NB y-tiles of 16 activation rows).
+template <typename T, int EPI, int NA, int NB>
+__device__ __forceinline__ void store_tile(const f32x4 (&acc)[NA][NB], const GemmParams& p, int m, int n) {
+  using V4 = typename GVec<T>::x4;
+  T* ob = static_cast<T*>(p.out);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int mb = m + 16 * b;
+    if (mb < p.M) {
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        if constexpr (EPI == CRAM_GEMM_STORE) {
+          V4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (T)acc[a][b][i];
+          *reinterpret_cast<V4*>(ob + (int64_t)mb * p.ldo + n + 16 * a) = v;
+        } else if ((a & 2) == 0) {
+          // gate tiles a = 0, 1 (mod 4) and their up tiles a + 2 (weight rows interleaved in blocks of 32): the gate
+          // column n' = n + 16 a is output column f = 32 * (n' / 64) + n' % 64
+          const int ng = n + 16 * a;
+          const int f = 32 * (ng >> 6) + (ng & 63);
+          V4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float g = rnd<T>(acc[a][b][i]), u = rnd<T>(acc[a + 2][b][i]);
+            const float sg = rnd<T>(g / (1.0f + expf(-g)));
+            v[i] = (T)(sg * u);
+          }
+          *reinterpret_cast<V4*>(ob + (int64_t)mb * p.ldo + f) = v;
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int EPI>
+__global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  int tm, tn;
+  tile_of(p, blockIdx.x, tm, tn);
+  const int n0 = tn * BN, m0 = tm * BM;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wx = wave >> 2, wy = wave & 3;
+
+  // buffer descriptors: x tile rows n0.., y tile rows m0.. (rows past M read as zeros)
+  const T* xb = static_cast<const T*>(p.x) + (int64_t)n0 * p.ldx;
+  const T* yb = static_cast<const T*>(p.y) + (int64_t)m0 * p.ldy;
+  const int yrows = min(BM, p.M - m0);
+  const auto xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, (int)((BN - 1) * p.ldx * 2 + p.K * 2),
+                                                      0x00020000);
+  const auto ysrd = __builtin_amdgcn_make_buffer_rsrc((void*)yb, (short)0, (int)((yrows - 1) * p.ldy * 2 + p.K * 2),
+                                                      0x00020000);
+
+  // LDS-DMA: unit u, instruction i of this wave writes 8 rows (1 KiB) starting at tile row R(u, 2*wave + i);
+  // lane L fetches row R + L/8, chunk (L%8) ^ swz(row)
+  const int lr = lane >> 3, ls = lane & 7;
+  uint32_t vx[2], vy[2];
+  int rx[2], ry[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = 2 * wave + i;
+    rx[i] = q < 8 ? 8 * q : 128 + 8 * (q - 8);                // x_lo unit rows (x_hi: +64)
+    ry[i] = (q >> 2) * 64 + 8 * (q & 3);                      // y_lo unit rows (y_hi: +32)
+    const int xr = rx[i] + lr, yr = ry[i] + lr;
+    vx[i] = (uint32_t)(xr * p.ldx * 2 + ((ls ^ ((xr >> 1) & 7)) * 16));
+    vy[i] = (uint32_t)(yr * p.ldy * 2 + ((ls ^ ((yr >> 1) & 7)) * 16));
+  }
+  const int xhi_off = (int)(64 * p.ldx * 2), yhi_off = (int)(32 * p.ldy * 2);
+  char* const sbase = smem;
+  auto stage_x = [&](int t, int hi) {          // x_lo (hi = 0) or x_hi (hi = 1) of K-tile t
+    char* img = sbase + (t & 1) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xsrd, (lds_void*)(img + (rx[i] + 64 * hi) * ROWB), 16, (int)vx[i],
+                                               t * ROWB + hi * xhi_off, 0, 0);
+  };
+  auto stage_y = [&](int t, int hi) {
+    char* img = sbase + (t & 1) * STAGE + IMG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ysrd, (lds_void*)(img + (ry[i] + 32 * hi) * ROWB), 16, (int)vy[i],
+                                               t * ROWB + hi * yhi_off, 0, 0);
+  };
+
+  // fragment reads: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row tile, k chunk 4 ks + g
+  const int fr = lane & 15, fg = lane >> 4;
+  uint32_t foff[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) foff[ks] = (uint32_t)(fr * ROWB + (((4 * ks + fg) ^ (fr >> 1)) * 16));
+  const int xrow0 = wx * 128, yrow0 = wy * 64;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 xf[4][2], ylo[2][2], yhi[2][2];   // [tile][ks]
+  auto read_x = [&](const char* img, int h) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        xf[a][ks] = *reinterpret_cast<const u32x4*>(img + (xrow0 + 64 * h + 16 * a) * ROWB + foff[ks]);
+  };
+  auto read_y = [&](const char* img, int h, u32x4 (&yf)[2][2]) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        yf[b][ks] = *reinterpret_cast<const u32x4*>(img + IMG + (yrow0 + 32 * h + 16 * b) * ROWB + foff[ks]);
+  };
+  auto mma = [&](int h, int yh, const u32x4 (&yf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[4 * h + a][2 * yh + b] = mfma16(xf[a][ks], yf[b][ks], acc[4 * h + a][2 * yh + b], T{});
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nt = p.K / BK;
+  // prologue: all of tile 0, and tile 1 except its x_hi unit (issued in tile 0's first phase)
+  stage_x(0, 0); stage_y(0, 0); stage_y(0, 1); stage_x(0, 1);
+  if (nt > 1) {
+    stage_x(1, 0); stage_y(1, 0); stage_y(1, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  barrier();
+  if (wx == 1) barrier();   // waves 4-7 run one interval behind
+
+  // one K-tile: S1 = a tile t+1 exists (stage its x_hi, wait for it), S2 = a tile t+2 exists (stage 3 units)
+  auto ktile = [&](int t, auto s1c, auto s2c) {
+    constexpr bool S1 = decltype(s1c)::value, S2 = decltype(s2c)::value;
+    const char* img = sbase + (t & 1) * STAGE;
+    // phase 0: x rows 0-63 of the wave, y rows 0-31
+    read_x(img, 0);
+    read_y(img, 0, ylo);
+    if constexpr (S1) stage_x(t + 1, 1);
+    barrier();
+    mma(0, 0, ylo);
+    barrier();
+    // phase 1: y rows 32-63
+    read_y(img, 1, yhi);
+    barrier();
+    mma(0, 1, yhi);
+    barrier();
+    // phase 2: x rows 64-127 (x_lo and y_lo of this stage were consumed in phase 0: restage them for t+2)
+    read_x(img, 1);
+    if constexpr (S2) { stage_x(t + 2, 0); stage_y(t + 2, 0); }
+    barrier();
+    mma(1, 1, yhi);
+    barrier();
+    // phase 3: no reads; y_hi (consumed in phase 1) restaged for t+2, then tile t+1 retired
+    if constexpr (S2) {
+      stage_y(t + 2, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else if constexpr (S1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    mma(1, 0, ylo);
+    barrier();
+  };
+  using TT = std::integral_constant<bool, true>;
+  using FF = std::integral_constant<bool, false>;
+  int t = 0;
+  for (; t + 2 < nt; ++t) ktile(t, TT{}, TT{});
+  if (t + 1 < nt) { ktile(t, TT{}, FF{}); ++t; }
+  ktile(t, FF{}, FF{});
+  if (wx == 0) barrier();   // equal barrier counts for both halves
+
+  // epilogue: lane (j, g) holds acc[a][b][i] = out[m0 + yrow0 + 16 b + j][n0 + xrow0 + 16 a + 4 g + i]
+  store_tile<T, EPI, 8, 4>(acc, p, m0 + yrow0 + fr, n0 + xrow0 + 4 * fg);
+}
+
+inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
+
+}  // namespace
+
+extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N,
+                         int K, int epilogue, int dtype, cram_stream_t stream) {
+  if (!y || !x || !out || M <= 0 || N <= 0 || K <= 0) return CRAM_ERR_INVALID_ARG;
+  if (epilogue != CRAM_GEMM_STORE && epilogue != CRAM_GEMM_SILU_MUL) return CRAM_ERR_INVALID_ARG;
+  if (dtype != CRAM_DTYPE_BF16 && dtype != CRAM_DTYPE_F16) return CRAM_ERR_UNSUPPORTED;
+  if (N % BN != 0 || K % BK != 0) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(y) || !al16(x) || !al16(out) || (ldy & 7) || (ldx & 7) || (ldo & 3)) return CRAM_ERR_ALIGNMENT;
+  const int nout = epilogue == CRAM_GEMM_STORE ? N : N / 2;
+  if (ldy < K || ldx < K || ldo < nout) return CRAM_ERR_INVALID_ARG;
+  // buffer-descriptor extents (one 256-row tile) are 32-bit byte counts
+  if ((int64_t)BN * ldx * 2 >= (1ll << 31) || (int64_t)BM * ldy * 2 >= (1ll << 31)) return CRAM_ERR_UNSUPPORTED;
+  GemmParams p;
+  p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo;
+  p.M = M; p.N = N; p.K = K;
+  p.ntm = (M + BM - 1) / BM;
+  p.ntn = N / BN;
+  const int64_t nb = (int64_t)p.ntm * p.ntn;
+  if (nb > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
+  p.nblocks = (int)nb;
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 g(p.nblocks);
+  const dim3 blk(512);
+  if (dtype == CRAM_DTYPE_BF16) {
+    if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<__bf16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
+    else hipLaunchKernelGGL((gemm_tn_kernel<__bf16, CRAM_GEMM_SILU_MUL>), g, blk, 0, st, p);
+  } else {
+    if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
+    else hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_SILU_MUL>), g, blk, 0, st, p);
+  }
+  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}

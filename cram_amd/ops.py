@@ -339,3 +339,41 @@ def silu_mul(gu: torch.Tensor, F: int, out: Optional[torch.Tensor] = None) -> to
                                      _dt(gu), _stream(gu.device))
     _lib.check(code, "cram_silu_mul")
     return out
+
+
+GEMM_STORE = 0      # CRAM_GEMM_STORE
+GEMM_SILU_MUL = 1   # CRAM_GEMM_SILU_MUL
+
+
+def interleave_gate_up(wgu: torch.Tensor, F: int) -> torch.Tensor:
+    """[gate; up] rows ([2F, K], gate_proj then up_proj) -> rows interleaved in blocks of 32 (64j..64j+31 = gate
+    32j.., 64j+32..64j+63 = up 32j..), the weight layout of cram_gemm's SiLU-mul epilogue."""
+    if wgu.dim() != 2 or wgu.shape[0] != 2 * F or F % 32:
+        raise ValueError(f"gate/up weight must be [2F, K] with F % 32 == 0, got {tuple(wgu.shape)}, F={F}")
+    K = wgu.shape[1]
+    return torch.stack([wgu[:F].reshape(F // 32, 32, K), wgu[F:].reshape(F // 32, 32, K)], 1).reshape(2 * F, K)
+
+
+def gemm(x: torch.Tensor, w: torch.Tensor, epilogue: int = GEMM_STORE, out: Optional[torch.Tensor] = None,
+         name: str = "cram_gemm") -> torch.Tensor:
+    """x [..., K] @ w[N, K]^T on the hand-written MFMA GEMM (cram_gemm); GEMM_SILU_MUL takes an interleaved gate/up
+    weight (interleave_gate_up) and returns the MLP activation [..., N/2]."""
+    _dt(x)
+    if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("w must be a [N, K] row-major weight of x's dtype")
+    x2 = _rows2d(x, "x")
+    M, K = x2.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"K mismatch: x {K}, w {w.shape[1]}")
+    nout = N if epilogue == GEMM_STORE else N // 2
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (nout,), dtype=x.dtype, device=x.device)
+    o2 = _rows2d(out, "out")
+    ev = TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout), x.device) if TIMER.enabled else None
+    code = _lib.load().cram_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(), o2.stride(0),
+                                 M, N, K, int(epilogue), _dt(x), _stream(x.device))
+    _lib.check(code, "cram_gemm")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(x.device))
+    return out

@@ -170,6 +170,21 @@ int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows
                   cram_stream_t stream);
 
 /*
+ * Projection GEMM of the engine (cram_gemm.hip; replaces F.linear / hipBLASLt for the MLP gate/up projection
+ * and its activation: re_weighting.py:158,170 run them as nn.Linear inside every hooked forward).
+ *   out[m, n] = sum_k y[m, k] * x[n, k]      y: activations [M][K] (row stride ldy), x: weights [N][K] (ldx),
+ *   fp32 accumulation, bf16 / fp16 in and out; N % 256 == 0, K % 64 == 0, 16-byte aligned rows, any M >= 1.
+ *   CRAM_GEMM_STORE      out [M][N] (ldo) = rnd(acc)
+ *   CRAM_GEMM_SILU_MUL   x is a gate/up weight with rows interleaved in blocks of 32 (rows 64j..64j+31 = gate rows
+ *                        32j.., rows 64j+32..64j+63 = up rows 32j..); out [M][N/2] (ldo):
+ *                        out[m, f] = rnd(rnd(silu(rnd(gate))) * rnd(up)), cram_silu_mul's arithmetic
+ */
+#define CRAM_GEMM_STORE 0
+#define CRAM_GEMM_SILU_MUL 1
+int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N, int K,
+              int epilogue, int dtype, cram_stream_t stream);
+
+/*
  * Host-side prompt -> credibility weights (cram_spans.cpp; no device, no stream), batched over B prompts.
  * Replaces the per-passage offset-mapping scan of re_weighting.py:100-111.
  *

@@ -94,6 +94,16 @@ static void validation_paths() {
   EXPECT(cram_silu_mul(f, 8, f, 8, 1, 16, 7, nullptr) == CRAM_ERR_UNSUPPORTED);
   EXPECT(cram_silu_mul(f, 8, f, 8, 1, 12, 0, nullptr) == CRAM_ERR_ALIGNMENT);
   EXPECT(cram_silu_mul(f, 8, f, 8, 0, 16, 0, nullptr) == CRAM_OK);
+  // projection GEMM: validated before any launch
+  EXPECT(cram_gemm(nullptr, 64, f, 64, f, 256, 1, 256, 64, CRAM_GEMM_STORE, 0, nullptr) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_gemm(f, 64, f, 64, f, 256, 0, 256, 64, CRAM_GEMM_STORE, 0, nullptr) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_gemm(f, 64, f, 64, f, 256, 1, 256, 64, 2, 0, nullptr) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_gemm(f, 64, f, 64, f, 256, 1, 256, 64, CRAM_GEMM_STORE, 5, nullptr) == CRAM_ERR_UNSUPPORTED);
+  EXPECT(cram_gemm(f, 64, f, 64, f, 256, 1, 200, 64, CRAM_GEMM_STORE, 0, nullptr) == CRAM_ERR_UNSUPPORTED);
+  EXPECT(cram_gemm(f, 48, f, 48, f, 256, 1, 256, 48, CRAM_GEMM_STORE, 0, nullptr) == CRAM_ERR_UNSUPPORTED);
+  EXPECT(cram_gemm(f, 68, f, 64, f, 256, 1, 256, 64, CRAM_GEMM_STORE, 0, nullptr) == CRAM_ERR_ALIGNMENT);
+  EXPECT(cram_gemm(f, 64, f, 64, f, 128, 1, 512, 64, CRAM_GEMM_STORE, 0, nullptr) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_gemm(f, 64, f, 64, f, 255, 1, 512, 64, CRAM_GEMM_SILU_MUL, 0, nullptr) == CRAM_ERR_ALIGNMENT);
   // error strings and knobs
   for (int c = 1; c >= -7; --c) EXPECT(cram_strerror(c) != nullptr && std::strlen(cram_strerror(c)) > 0);
   EXPECT(cram_abi_version() == CRAM_ABI_VERSION);

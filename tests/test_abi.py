@@ -17,7 +17,8 @@ def _declared():
 def test_header_declares_the_boundary():
     names = _declared()
     for n in ("cram_attn_prefill", "cram_attn_decode", "cram_attn_decode_workspace_size", "cram_answer_logits",
-              "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_rope_split", "cram_silu_mul"):
+              "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_rope_split", "cram_silu_mul",
+              "cram_gemm"):
         assert n in names
 
 
@@ -58,6 +59,12 @@ def test_argument_validation_without_gpu():
                               1, 1, 1, 4, None, 128, 1.0, None, 0, None, 0, 0, 4, None, 0, 0, None) == -5
     assert L.cram_rmsnorm(None, 0, None, 0, None, 0, None, None, 0, 1, 8, 1e-5, 0, None) == -1
     assert L.cram_silu_mul(fake, 8, fake, 8, 1, 12, 0, None) == -3
+    # projection GEMM: N % 256, K % 64, row alignment, epilogue code, output row length
+    assert L.cram_gemm(fake, 64, fake, 64, fake, 256, 1, 200, 64, 0, 0, None) == -2
+    assert L.cram_gemm(fake, 48, fake, 48, fake, 256, 1, 256, 48, 0, 0, None) == -2
+    assert L.cram_gemm(fake, 68, fake, 64, fake, 256, 1, 256, 64, 0, 0, None) == -3
+    assert L.cram_gemm(fake, 64, fake, 64, fake, 256, 1, 256, 64, 2, 0, None) == -1
+    assert L.cram_gemm(fake, 64, fake, 64, fake, 128, 1, 512, 64, 0, 0, None) == -1
 
 
 def test_kernel_knobs_latch_without_gpu():
