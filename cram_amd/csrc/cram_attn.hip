@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "../../include/cram_attn.h"
 
 namespace {
@@ -38,6 +40,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 typedef __attribute__((address_space(3))) void lds_void;
@@ -303,21 +306,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
   // writes 1 KiB of the padded (K | V) image of a tile = 64 lanes x 16 B; lane p of chunk c fetches
   // the 16 bytes that belong at image offset c*1024 + 16p (a pad slot gets an out-of-range offset, so
   // the descriptor's range check writes zeros there, as it does for rows past key S).
-  constexpr int KCH = C::KCH, NCH = C::KCH + C::VCH;
-  constexpr int CPW = (NCH + NW - 1) / NW;     // chunks per wave per tile
-  uint32_t doff[CPW];
+  // chunks of the K image are c = wave + NW i (i < KPW), then those of the V image likewise: only a wave's last chunk
+  // of each image can fall past it, so the K-or-V choice is compile-time (a per-chunk runtime choice keeps ~40
+  // scalar lane conditions live)
+  constexpr int KCH = C::KCH, VCH = C::VCH;
+  constexpr int KPW = (KCH + NW - 1) / NW, VPW = (VCH + NW - 1) / NW;
+  uint32_t dk[KPW], dv[VPW];
 #pragma unroll
-  for (int i = 0; i < CPW; ++i) {
-    const int c = wave + NW * i;
-    uint32_t off = 0xFFFFFFF0u;
-    if (c < KCH) {
-      const int x = c * 1024 + 16 * lane, row = x / C::KSTR, colb = x % C::KSTR;
-      if (x < C::K_BYTES && colb < D * 2) off = (uint32_t)(row * p.k_st * 2 + colb);
-    } else if (c < NCH) {
-      const int x = (c - KCH) * 1024 + 16 * lane, row = x / C::VSTR, colb = x % C::VSTR;
-      if (x < C::V_BYTES && colb < D * 2) off = (uint32_t)(row * p.v_st * 2 + colb);
-    }
-    doff[i] = off;
+  for (int i = 0; i < KPW; ++i) {
+    const int x = (wave + NW * i) * 1024 + 16 * lane, row = x / C::KSTR, colb = x % C::KSTR;
+    dk[i] = (x < C::K_BYTES && colb < D * 2) ? (uint32_t)(row * p.k_st * 2 + colb) : 0xFFFFFFF0u;
+  }
+#pragma unroll
+  for (int i = 0; i < VPW; ++i) {
+    const int x = (wave + NW * i) * 1024 + 16 * lane, row = x / C::VSTR, colb = x % C::VSTR;
+    dv[i] = (x < C::V_BYTES && colb < D * 2) ? (uint32_t)(row * p.v_st * 2 + colb) : 0xFFFFFFF0u;
   }
   float bst = 0.f;
 
@@ -330,12 +333,17 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
                                                         (int)((rows_left - 1) * p.v_st * 2 + D * 2), 0x00020000);
     char* base = smem + (t & 1) * C::STAGE;
 #pragma unroll
-    for (int i = 0; i < CPW; ++i) {
+    for (int i = 0; i < KPW; ++i) {
       const int c = wave + NW * i;
-      if (c < KCH)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (lds_void*)(base + c * 1024), 16, (int)doff[i], 0, 0, 0);
-      else if (c < NCH)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(vsrd, (lds_void*)(base + c * 1024), 16, (int)doff[i], 0, 0, 0);
+      if ((i + 1) * NW <= KCH || c < KCH)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ksrd, (lds_void*)(base + c * 1024), 16, (int)dk[i], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < VPW; ++i) {
+      const int c = wave + NW * i;
+      if ((i + 1) * NW <= VCH || c < VCH)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vsrd, (lds_void*)(base + C::V_OFF + c * 1024), 16, (int)dv[i], 0, 0,
+                                                 0);
     }
     if (en_any && tid < C::BK) {
       const int wl = p.W - key0;
@@ -374,7 +382,12 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
 #ifdef CRAM_STAMPS
   unsigned long long st_[6] = {}, acc_[7] = {};
 #endif
-  for (int t = 0; t < nt; ++t) {
+  // One K/V tile with NB 32-key MFMA blocks: C::NKB, or 1 for the workgroup's last tile when its upper 32 keys lie
+  // past every row's causal / length limit (kv_end <= key0 + 32: the block would be all -inf; skipping it removes
+  // the fully masked MFMAs of half the diagonal tiles).  Score arithmetic on pairs (v_pk_fma_f32 / v_pk_add_f32):
+  // per element the same fma as before, row sums as two interleaved partial sums.
+  auto tile = [&](int t, auto nbc) {
+    constexpr int NB = decltype(nbc)::value;
     CRAM_STAMP(0)
     if (t + 1 < nt) gload(t + 1);
     const int key0 = t * C::BK;
@@ -383,7 +396,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
       f32x16 sacc[C::NKB];
       const f32x16 zero16 = {};
 #pragma unroll
-      for (int kb = 0; kb < C::NKB; ++kb) {
+      for (int kb = 0; kb < NB; ++kb) {
 #pragma unroll
         for (int ks = 0; ks < D / 16; ++ks) {
           const V8 a = *reinterpret_cast<const V8*>(base + (kb * 32 + r) * C::KSTR + (16 * ks + 8 * hh) * 2);
@@ -393,14 +406,15 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
       // scores (log2 units): scale, credibility bias, causal / length mask.  Wave-uniform split: a tile
       // with no masked key and no bias keeps the raw scores (max of raw scores, then one scaled max:
       // fl(c*s) is monotone in s, so it equals the max of the scaled scores) and folds the scale into
-      // the exponent's FMA — 3.5 VALU per score instead of 7.
+      // the exponent's FMA.
       const float* bl = reinterpret_cast<const float*>(base + C::B_OFF);
-      const bool need_mask = (key0 + C::BK - 1 > wave_qpos_min) || (key0 + C::BK > S);
+      const bool need_mask = (key0 + 32 * NB - 1 > wave_qpos_min) || (key0 + 32 * NB > S);
       const bool plain = !need_mask && !en;
+      const f32x2 c2 = {p.scale_log2, p.scale_log2};
       float mx = kNegInf;
       if (plain) {
 #pragma unroll
-        for (int kb = 0; kb < C::NKB; ++kb)
+        for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
           for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sacc[kb][e]);
         mx *= p.scale_log2;
@@ -408,29 +422,37 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
         // raw scores stay in sacc: the exponent below is fma(s, c, b - m), which for b == 0 is exactly
         // the plain path's fma(s, c, -m) (a zero bias is bit-identical to no bias)
 #pragma unroll
-        for (int kb = 0; kb < C::NKB; ++kb) {
+        for (int kb = 0; kb < NB; ++kb) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + kb * 32 + 8 * g + 4 * hh);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) mx = fmaxf(mx, __builtin_fmaf(sacc[kb][4 * g + e], p.scale_log2, bv[e]));
+            for (int e = 0; e < 4; e += 2) {
+              const f32x2 sv = {sacc[kb][4 * g + e], sacc[kb][4 * g + e + 1]};
+              const f32x2 v = __builtin_elementwise_fma(sv, c2, f32x2{bv[e], bv[e + 1]});
+              mx = fmaxf(mx, fmaxf(v[0], v[1]));
+            }
           }
         }
       } else {                                                   // diagonal / ragged tile
         const int lim = min(qpos, S - 1) - key0;
 #pragma unroll
-        for (int kb = 0; kb < C::NKB; ++kb) {
+        for (int kb = 0; kb < NB; ++kb) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             f32x4 bv = {0.f, 0.f, 0.f, 0.f};
             if (en) bv = *reinterpret_cast<const f32x4*>(bl + kb * 32 + 8 * g + 4 * hh);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float s = __builtin_fmaf(sacc[kb][4 * g + e], p.scale_log2, bv[e]);
+            for (int e = 0; e < 4; e += 2) {
+              const f32x2 sv = {sacc[kb][4 * g + e], sacc[kb][4 * g + e + 1]};
+              f32x2 v = __builtin_elementwise_fma(sv, c2, f32x2{bv[e], bv[e + 1]});
               // branch-free causal / length mask: key offset in tile vs the lane's last allowed key
-              s = (kb * 32 + 8 * g + 4 * hh + e > lim) ? kNegInf : s;
-              sacc[kb][4 * g + e] = s;
-              mx = fmaxf(mx, s);
+              const int col = kb * 32 + 8 * g + 4 * hh + e;
+              v[0] = (col > lim) ? kNegInf : v[0];
+              v[1] = (col + 1 > lim) ? kNegInf : v[1];
+              sacc[kb][4 * g + e] = v[0];
+              sacc[kb][4 * g + e + 1] = v[1];
+              mx = fmaxf(mx, fmaxf(v[0], v[1]));
             }
           }
         }
@@ -440,33 +462,43 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
       const float mnew = fmaxf(m, mx);
       const float muse = (mnew == kNegInf) ? 0.f : mnew;
       const float alpha = fast_exp2(m - muse);
-      float rs = 0.f;
+      f32x2 rs2 = {0.f, 0.f};
+      const f32x2 nm2 = {-muse, -muse};
       if (!plain && !need_mask) {
 #pragma unroll
-        for (int kb = 0; kb < C::NKB; ++kb)
+        for (int kb = 0; kb < NB; ++kb)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + kb * 32 + 8 * g + 4 * hh);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float pe = fast_exp2(__builtin_fmaf(sacc[kb][4 * g + e], p.scale_log2, bv[e] - muse));
-              sacc[kb][4 * g + e] = pe;
-              rs += pe;
+            for (int e = 0; e < 4; e += 2) {
+              const f32x2 sv = {sacc[kb][4 * g + e], sacc[kb][4 * g + e + 1]};
+              f32x2 v = __builtin_elementwise_fma(sv, c2, f32x2{bv[e], bv[e + 1]} + nm2);
+              v[0] = fast_exp2(v[0]);
+              v[1] = fast_exp2(v[1]);
+              sacc[kb][4 * g + e] = v[0];
+              sacc[kb][4 * g + e + 1] = v[1];
+              rs2 += v;
             }
           }
       } else {
         const float sc = plain ? p.scale_log2 : 1.f;
+        const f32x2 sc2 = {sc, sc};
 #pragma unroll
-        for (int kb = 0; kb < C::NKB; ++kb) {
+        for (int kb = 0; kb < NB; ++kb) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const float pe = fast_exp2(__builtin_fmaf(sacc[kb][e], sc, -muse));
-            sacc[kb][e] = pe;
-            rs += pe;
+          for (int e = 0; e < 16; e += 2) {
+            const f32x2 sv = {sacc[kb][e], sacc[kb][e + 1]};
+            f32x2 v = __builtin_elementwise_fma(sv, sc2, nm2);
+            v[0] = fast_exp2(v[0]);
+            v[1] = fast_exp2(v[1]);
+            sacc[kb][e] = v[0];
+            sacc[kb][e + 1] = v[1];
+            rs2 += v;
           }
         }
       }
-      rs = half_sum(rs);
+      const float rs = half_sum(rs2[0] + rs2[1]);
       CRAM_STAMP(2)
       l = l * alpha + rs;
       m = mnew;
@@ -484,10 +516,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
       if constexpr (D == 128) {     // V^T reads by inline asm (tr_reads32): the K/V prefetch stays in flight
         const uint32_t vaddr = (uint32_t)(uintptr_t)(const lds_void*)vimg + (uint32_t)(tr_key * C::VSTR + tr_col * 2);
         pv_block32<T, C::VSTR, 0>(vaddr, sacc[0], oacc);
-        if constexpr (C::NKB == 2) pv_block32<T, C::VSTR, 1>(vaddr, sacc[1], oacc);
+        if constexpr (NB == 2) pv_block32<T, C::VSTR, 1>(vaddr, sacc[1], oacc);
       } else
 #pragma unroll
-      for (int kb = 0; kb < C::NKB; ++kb) {
+      for (int kb = 0; kb < NB; ++kb) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           V8 pb;
@@ -523,7 +555,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
     }
     st_[1] = 0;
 #endif
-  }
+  };
+  const bool half_last = C::NKB == 2 && nt > 0 && kv_end <= (nt - 1) * C::BK + 32;
+  const int nfull = half_last ? nt - 1 : nt;
+  for (int t = 0; t < nfull; ++t) tile(t, std::integral_constant<int, C::NKB>{});
+  if (half_last) tile(nt - 1, std::integral_constant<int, 1>{});
 
 #ifdef CRAM_STAMPS
   if (lane == 0)
