@@ -66,8 +66,11 @@ def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, i
     ms = s.elapsed_time(e) / iters
     kv_bytes = float(sum(sess.lens)) * sp.num_kv_heads * sp.head_dim * 2 * 2
     ach = kv_bytes / (ms * 1e-3) / 1e9
+    G = sp.num_heads // sp.num_kv_heads
+    kern = ("decode_mfma_kernel (16x16x32 matrix cores, GQA group of %d)" % G if G >= 4 and sp.head_dim == 128
+            else "decode_kernel (VALU)") + (" + decode_combine_kernel (split %d)" % sess.splits if sess.splits > 1 else "")
     res = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-           "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": "decode_kernel (+ decode_combine_kernel when split)",
+           "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": kern,
            "avg_launch_ms": round(ms, 4), "bytes_per_launch": kv_bytes, "batch": sess.B, "splits": sess.splits,
            "note": "layer 0 of the decode leg's prefilled KV cache, timed apart from the decode leg"}
     del sess
