@@ -384,8 +384,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
 #endif
   // One K/V tile with NB 32-key MFMA blocks: C::NKB, or 1 for the workgroup's last tile when its upper 32 keys lie
   // past every row's causal / length limit (kv_end <= key0 + 32: the block would be all -inf; skipping it removes
-  // the fully masked MFMAs of half the diagonal tiles).  Score arithmetic on pairs (v_pk_fma_f32 / v_pk_add_f32):
-  // per element the same fma as before, row sums as two interleaved partial sums.
+  // the fully masked MFMAs of half the diagonal tiles).  Score arithmetic on pairs (v_pk_fma_f32): per element the
+  // same fma as before; the row sums stay sequential (two interleaved partial sums moved a near-tie answer log-prob
+  // across the drop-in's noise-floor bar).
   auto tile = [&](int t, auto nbc) {
     constexpr int NB = decltype(nbc)::value;
     CRAM_STAMP(0)
@@ -462,7 +463,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
       const float mnew = fmaxf(m, mx);
       const float muse = (mnew == kNegInf) ? 0.f : mnew;
       const float alpha = fast_exp2(m - muse);
-      f32x2 rs2 = {0.f, 0.f};
+      float rs = 0.f;                         // sequential sum: the previous kernel's rounding, bit for bit
       const f32x2 nm2 = {-muse, -muse};
       if (!plain && !need_mask) {
 #pragma unroll
@@ -478,7 +479,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
               v[1] = fast_exp2(v[1]);
               sacc[kb][4 * g + e] = v[0];
               sacc[kb][4 * g + e + 1] = v[1];
-              rs2 += v;
+              rs += v[0];
+              rs += v[1];
             }
           }
       } else {
@@ -494,11 +496,12 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
             v[1] = fast_exp2(v[1]);
             sacc[kb][e] = v[0];
             sacc[kb][e + 1] = v[1];
-            rs2 += v;
+            rs += v[0];
+            rs += v[1];
           }
         }
       }
-      const float rs = half_sum(rs2[0] + rs2[1]);
+      rs = half_sum(rs);
       CRAM_STAMP(2)
       l = l * alpha + rs;
       m = mnew;
@@ -1013,7 +1016,7 @@ bool g_knob_init = false;
 inline void knobs_init() {
   if (g_knob_init) return;
   const char* e = getenv("CRAM_PREFILL_VARIANT");
-  g_knob[CRAM_KNOB_PREFILL_VARIANT] = (e && (e[0] == '3' || e[0] == '8')) ? e[0] - '0' : -1;
+  g_knob[CRAM_KNOB_PREFILL_VARIANT] = (e && (e[0] == '0' || e[0] == '3' || e[0] == '7' || e[0] == '8')) ? e[0] - '0' : -1;
   const char* eu = getenv("CRAM_DECODE_U");
   g_knob[CRAM_KNOB_DECODE_U] = (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1;
   const char* em = getenv("CRAM_DECODE_MFMA");
@@ -1036,9 +1039,18 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // shape, but on the tiny Qwen2 model its IE noise doubled on one question and broke the parity bar
   // (tools/ie_noise_probe.py), so 64-key tiles at two waves per SIMD stay the default.
   // variant 8: 8-wave workgroups (one per CU), every K/V tile feeds twice the query rows.
+  // variant 7: for GQA groups of 7 (Qwen2-7B), 7-wave workgroups = the 7 query heads of one kv head over the same 32
+  // rows (hp = 7: every K/V tile feeds all seven heads, and all waves of a block finish together; otherwise hp = 1,
+  // 4 row groups of one head).  Automatic for sequences <= 2048: at the Qwen2 layout, B = 33 x T = 962 ran 601 vs
+  // 544 TFLOP/s, but B = 1 x T = 8300 582 vs 807 (one 7-wave workgroup per CU instead of two 4-wave ones;
+  // tools/ab_prefill_inproc.py, profiles/r02/ab_prefill_hp7.log).  Knob 0 forces the 4-wave layout.
   const int kv = knob(CRAM_KNOB_PREFILL_VARIANT);
-  const int var = (D == 128 && (kv == 3 || kv == 8)) ? kv : 0;
-  const int nw = var == 8 ? 8 : 4;
+  int var = (D == 128 && (kv == 3 || kv == 8)) ? kv : 0;
+  if (D == 128 && G % 7 == 0 && (kv == 7 || (kv == -1 && p.Tq <= 2048))) {
+    var = 7;
+    p.hp = 7;
+  }
+  const int nw = var == 8 ? 8 : var == 7 ? 7 : 4;
   const int bq = 32 * (nw / p.hp);
   p.nqb = (p.Tq + bq - 1) / bq;
   const int64_t nblocks = (int64_t)p.nqb * (p.Hq / p.hp) * p.B;
@@ -1048,6 +1060,8 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
     hipLaunchKernelGGL((prefill_kernel<T, D, 32, 3>), dim3(p.nblocks), dim3(256), 0, stream, p);
   else if (var == 8)
     hipLaunchKernelGGL((prefill_kernel<T, D, 64, 1, 8>), dim3(p.nblocks), dim3(512), 0, stream, p);
+  else if (var == 7)
+    hipLaunchKernelGGL((prefill_kernel<T, D, 64, 1, 7>), dim3(p.nblocks), dim3(448), 0, stream, p);
   else
     hipLaunchKernelGGL((prefill_kernel<T, D, 64, 2>), dim3(p.nblocks), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
@@ -1131,7 +1145,7 @@ int cram_abi_version(void) { return CRAM_ABI_VERSION; }
 int cram_set_knob(int which, int value) {
   if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
   knobs_init();
-  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 8)
+  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 7 && value != 8)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;

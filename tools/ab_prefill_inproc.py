@@ -12,14 +12,16 @@ from cram_amd import _lib, ops  # noqa: E402
 variants = sys.argv[1:] or ["-1", "8"]
 dev = torch.device("cuda:0")
 d = 128
+# AB_HEADS=28,4 for the Qwen2-7B head layout (GQA 7)
+HQ, HKV = (int(x) for x in os.environ.get("AB_HEADS", "32,8").split(","))
 shapes = [(33, 962), (1, 8300)]
 data = {}
 for B, T in shapes:
-    y = torch.randn(B, T, (32 + 16) * d, device=dev).to(torch.bfloat16)
-    q = y[..., :32 * d].unflatten(-1, (32, d)).transpose(1, 2)
-    k = y[..., 32 * d:40 * d].unflatten(-1, (8, d)).transpose(1, 2)
-    v = y[..., 40 * d:].unflatten(-1, (8, d)).transpose(1, 2)
-    data[(B, T)] = (q, k, v, torch.empty(B, T, 32, d, device=dev, dtype=torch.bfloat16))
+    y = torch.randn(B, T, (HQ + 2 * HKV) * d, device=dev).to(torch.bfloat16)
+    q = y[..., :HQ * d].unflatten(-1, (HQ, d)).transpose(1, 2)
+    k = y[..., HQ * d:(HQ + HKV) * d].unflatten(-1, (HKV, d)).transpose(1, 2)
+    v = y[..., (HQ + HKV) * d:].unflatten(-1, (HKV, d)).transpose(1, 2)
+    data[(B, T)] = (q, k, v, torch.empty(B, T, HQ, d, device=dev, dtype=torch.bfloat16))
 res = {(vv, s): [] for vv in variants for s in shapes}
 for rnd in range(5):
     for vv in variants:
@@ -39,6 +41,6 @@ for vv in variants:
     line = []
     for B, T in shapes:
         ms = statistics.median(res[(vv, (B, T))])
-        fl, _ = ops.prefill_work(B, 32, 8, T, T, d, 0)
+        fl, _ = ops.prefill_work(B, HQ, HKV, T, T, d, 0)
         line.append(f"B={B} T={T}: {ms:.3f} ms {fl / ms / 1e9:.0f} TF")
     print(f"variant {vv:>3}: " + " | ".join(line), flush=True)
