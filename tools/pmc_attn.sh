@@ -3,7 +3,7 @@
 set -e
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/pmc
+OUT=${OUT:-$R/gpurun_out/pmc}
 mkdir -p $OUT
 ARGS="${@:-}"
 run() {
