@@ -573,6 +573,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
                      static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh, p.o_st, q_row0, 1, Tq);
 }
 
+// one-wave-per-SIMD prefill (64 rows per wave, hand-ordered MFMA / softmax stream): prefill_x64_kernel
+#include "prefill_x64.inc"
+
 // --------------------------------------------------------------------------------------------
 // decode (q_len == 1)
 // --------------------------------------------------------------------------------------------
@@ -1016,7 +1019,8 @@ bool g_knob_init = false;
 inline void knobs_init() {
   if (g_knob_init) return;
   const char* e = getenv("CRAM_PREFILL_VARIANT");
-  g_knob[CRAM_KNOB_PREFILL_VARIANT] = (e && (e[0] == '0' || e[0] == '3' || e[0] == '7' || e[0] == '8')) ? e[0] - '0' : -1;
+  g_knob[CRAM_KNOB_PREFILL_VARIANT] =
+      (e && (e[0] == '0' || e[0] == '3' || e[0] == '6' || e[0] == '7' || e[0] == '8')) ? e[0] - '0' : -1;
   const char* eu = getenv("CRAM_DECODE_U");
   g_knob[CRAM_KNOB_DECODE_U] = (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1;
   const char* em = getenv("CRAM_DECODE_MFMA");
@@ -1045,6 +1049,18 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // 544 TFLOP/s, but B = 1 x T = 8300 582 vs 807 (one 7-wave workgroup per CU instead of two 4-wave ones;
   // tools/ab_prefill_inproc.py, profiles/r02/ab_prefill_hp7.log).  Knob 0 forces the 4-wave layout.
   const int kv = knob(CRAM_KNOB_PREFILL_VARIANT);
+  // variant 6: prefill_x64_kernel (one wave per SIMD, 64 rows per wave; bf16, d = 128, GQA groups of 4k)
+  if constexpr (D == 128 && std::is_same<T, __bf16>::value) {
+    if (kv == 6 && G % 4 == 0) {
+      p.hp = 4;
+      p.nqb = (p.Tq + 63) / 64;
+      const int64_t nb = (int64_t)p.nqb * (p.Hq / 4) * p.B;
+      if (nb > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
+      p.nblocks = (int)nb;
+      hipLaunchKernelGGL(prefill_x64_kernel, dim3(p.nblocks), dim3(256), 0, stream, p);
+      return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+    }
+  }
   int var = (D == 128 && (kv == 3 || kv == 8)) ? kv : 0;
   if (D == 128 && G % 7 == 0 && (kv == 7 || (kv == -1 && p.Tq <= 2048))) {
     var = 7;
@@ -1145,7 +1161,8 @@ int cram_abi_version(void) { return CRAM_ABI_VERSION; }
 int cram_set_knob(int which, int value) {
   if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
   knobs_init();
-  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 7 && value != 8)
+  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 6 && value != 7 &&
+      value != 8)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;
