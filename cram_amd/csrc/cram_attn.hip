@@ -1049,9 +1049,12 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // 544 TFLOP/s, but B = 1 x T = 8300 582 vs 807 (one 7-wave workgroup per CU instead of two 4-wave ones;
   // tools/ab_prefill_inproc.py, profiles/r02/ab_prefill_hp7.log).  Knob 0 forces the 4-wave layout.
   const int kv = knob(CRAM_KNOB_PREFILL_VARIANT);
-  // variant 6: prefill_x64_kernel (one wave per SIMD, 64 rows per wave; bf16, d = 128, GQA groups of 4k)
+  // variant 6: prefill_x64_kernel (one wave per SIMD, 64 rows per wave; bf16, d = 128, GQA groups of 4k).  Automatic
+  // from 4096 query rows (config 5's 8.3k-token prompts: 1.04-1.09x, tools/ab_x64.hip); shorter sequences keep the
+  // two-workgroups-per-CU kernel, which hides each block's prologue and store tail behind the co-resident one (x64 runs
+  // 0.80-0.88x at the IE-sweep shape, B = 33 x T = 962)
   if constexpr (D == 128 && std::is_same<T, __bf16>::value) {
-    if (kv == 6 && G % 4 == 0) {
+    if ((kv == 6 || (kv == -1 && p.Tq >= 4096)) && G % 4 == 0) {
       p.hp = 4;
       p.nqb = (p.Tq + 63) / 64;
       const int64_t nb = (int64_t)p.nqb * (p.Hq / 4) * p.B;

@@ -64,7 +64,8 @@ int cram_abi_version(void);
  * the first query; no launch reads the environment.  Not synchronised: set knobs before launching from other
  * threads.
  *   CRAM_KNOB_PREFILL_VARIANT  -1 = automatic: 64-key tiles, 4 waves, except GQA-7 groups with sequences <= 2048
- *                              (7-wave workgroups); 0 = always 4 waves; 3 = 32-key tiles; 8 = 8-wave workgroups;
+ *                              (7-wave workgroups) and bf16 GQA groups of 4k with >= 4096 query rows (variant 6);
+ *                              0 = always 4 waves; 3 = 32-key tiles; 8 = 8-wave workgroups;
  *                              7 = 7-wave workgroups for GQA-7 groups; 6 = one wave per SIMD, 64 rows per wave
  *                              (bf16, d = 128, GQA groups of 4k; otherwise as 0)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
