@@ -73,6 +73,21 @@ def test_cal_logits_matches_reference(fbh, nq, kind):
         ie_tolerance_check(ie, g["ie"], truth[g["idx"]])
 
 
+@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+def test_cal_logits_bf16_logits_match_reference(fbh, nq, kind):
+    """round_logits=True (each answer logit rounded to the model dtype, as transformers 5.15 returns them) against
+    the reference run under the same convention (G4 'bf16' variant, re_weighting.py:159-160,170), same bar."""
+    gold = [x for x in _load("tiny_ie.json.gz") if x["kind"] == kind and x["variant"] == "bf16"]
+    truth = {x["idx"]: x["ie"] for x in _load("tiny_ie_f32.json.gz") if x["kind"] == kind}
+    assert gold
+    obj = fbh[kind]
+    for g in gold:
+        rec = nq[g["idx"]]
+        ie = obj.cal_logits_tensor(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
+                                   scores=[0, 1, 1, 1, 1], wrong_answer=rec["wrong_answer"], round_logits=True)
+        ie_tolerance_check(ie.double().cpu().numpy(), g["ie"], truth[g["idx"]])
+
+
 def test_cal_logits_deterministic(fbh, nq):
     rec = nq[3]
     args = dict(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"], scores=[0, 1, 1, 1, 1],

@@ -5,7 +5,8 @@ REV=${1:-HEAD}
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
 mkdir -p $T/cram_amd/csrc $T/include
-for f in cram_amd/csrc/cram_attn.hip cram_amd/csrc/cram_fused.hip cram_amd/csrc/cram_spans.cpp include/cram_attn.h; do
+for f in cram_amd/csrc/cram_attn.hip cram_amd/csrc/cram_fused.hip cram_amd/csrc/cram_spans.cpp include/cram_attn.h \
+         $(git -C $R ls-tree --name-only $REV cram_amd/csrc/ | grep "\.inc$"); do
   git -C $R show $REV:$f > $T/$f
 done
 SRCS="$T/cram_amd/csrc/cram_attn.hip $T/cram_amd/csrc/cram_fused.hip $T/cram_amd/csrc/cram_spans.cpp"
