@@ -5,7 +5,10 @@ M = 33 x T rows is 9-12 % slower than the best solution TunableOp finds (`tools/
 A/B: 8.86 -> 8.55 ms per Llama-3-8B layer at M = 29184).  Tuning online is not an option (every question has
 its own M = 33 x T rounded to 256), so the solutions tuned once are pinned for every M the sweep and the packed
 prefill can produce: a TunableOp results file is written at start-up with one line per (N, K, M) and read
-back with tuning off.  Shapes without a line (decode steps, other models) run the default heuristic.
+back with tuning off.  The decode steps' weight-streaming GEMMs (M = batch rows: 256 for configs 2 / 4, 16 for
+config 5) get exact (N, K, M) lines where the tuned pick beat the default by >= 5 % in a same-process probe
+(`tools/tune_decode_gemms.py`, `decode_solutions`); they act inside the step graph's capture.  Shapes without a
+line (other models, other M) run the default heuristic.
 
 The solution ids belong to one hipBLASLt / rocBLAS build: the file carries the validators of the build they
 were tuned on (`data/gemm_solutions.json`), and nothing is pinned when the running build differs.
@@ -59,6 +62,9 @@ def install(m_values: Iterable[int], dtype: str = "BFloat16", path: str = SOLUTI
         N, K = (int(x) for x in key.split("x"))
         for M in m_values:
             lines.append(f"GemmTunableOp_{dtype}_TN,{_signature(N, K, M)},{name},0")
+    for key, name in sol.get("decode_solutions", {}).items():     # decode steps: exact (N, K, M = batch rows)
+        N, K, M = (int(x) for x in key.split("x"))
+        lines.append(f"GemmTunableOp_{dtype}_TN,{_signature(N, K, M)},{name},0")
     fd, fn = tempfile.mkstemp(prefix="cram_gemm_", suffix=".csv")
     with os.fdopen(fd, "w") as f:
         f.write("\n".join(lines) + "\n")

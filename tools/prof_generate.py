@@ -21,22 +21,26 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=256)
 ap.add_argument("--new", type=int, default=16)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--model", default="llama3-8b", choices=["llama3-8b", "qwen2-7b"],
+                help="llama3-8b: config 2 (NQ, top-894 heads); qwen2-7b: config 4 (TriviaQA, all heads)")
 a = ap.parse_args()
 
 dev = torch.device("cuda:0")
 configure_blas("hipblaslt")
-spec = ModelSpec.llama3_8b()
-eng = CrAMEngine.random(spec, dev, seed=1234, rope_theta=500000.0)
+qwen = a.model == "qwen2-7b"
+spec = ModelSpec.qwen2_7b() if qwen else ModelSpec.llama3_8b()
+eng = CrAMEngine.random(spec, dev, seed=1234, rope_theta=1e6 if qwen else 500000.0)
 from transformers import AutoTokenizer  # noqa: E402
 import gzip  # noqa: E402
-tok = AutoTokenizer.from_pretrained(os.path.join(REPO, "data", "tok_llama3"))
-data = json.load(gzip.open(os.path.join(REPO, "data", "nq_1000.json.gz"), "rt", encoding="utf-8"))
-heads = json.load(open(os.path.join(REPO, "data", "selected_heads.json")))["nq__llama3"]["heads"]
+tok = AutoTokenizer.from_pretrained(os.path.join(REPO, "data", "tok_qwen" if qwen else "tok_llama3"))
+data = json.load(gzip.open(os.path.join(REPO, "data", ("trivia" if qwen else "nq") + "_1000.json.gz"), "rt",
+                           encoding="utf-8"))
+heads = {} if qwen else json.load(open(os.path.join(REPO, "data", "selected_heads.json")))["nq__llama3"]["heads"]
 qs, ps, ss = [], [], []
 for j in range(a.B):
     paras, sc = scores.assemble(data[j], ideal=True, ideal_score=1)
     qs.append(data[j]["question"]); ps.append(paras); ss.append(sc)
-encs = spans.encode_batch(tok, "Meta-Llama-3-8B-Instruct", qs, ps, ss)
+encs = spans.encode_batch(tok, "Qwen2-7B-Instruct" if qwen else "Meta-Llama-3-8B-Instruct", qs, ps, ss)
 prompts = [ids.to(dev) for ids, _, _ in encs]
 ws = [w for _, w, _ in encs]
 
