@@ -154,32 +154,41 @@ __device__ __forceinline__ void pv_block32(uint32_t vaddr, const f32x16& pk, f32
 // Epilogue of the prefill kernels: the wave's 32 output rows (lane (r, hh) holds row r's columns
 // db*32 + 8g + 4hh .. +3) are staged through LDS as model-dtype rows (2D bytes each) and stored as 16-byte
 // pieces of whole rows, 4 rows of d = 128 per instruction, instead of 16 scattered 8-byte stores per lane (the
-// store tail is issue-bound: MI355X_MICROARCH.md, attention epilogue).  Staging row i is output row
-// first_row + i * row_step; rows >= Tq are not stored.
+// store tail is issue-bound: MI355X_MICROARCH.md, attention epilogue).  Staging row i is output row first_row + i.
+// The 1/l scaling runs on pairs (v_pk_mul_f32; per element the same product), and the stores go through a buffer
+// descriptor that ends at the last row < Tq: rows past it are dropped by the range check (no per-row branch, no
+// 64-bit address per store), the row offset of store i is a compile-time multiple of the row stride.
 template <typename T, int D>
 __device__ __forceinline__ void store_o_rows(char* stage, const f32x16 (&oacc)[D / 32], float inv, int r, int hh,
-                                             int lane, T* obase, int64_t o_st, int first_row, int row_step, int Tq) {
+                                             int lane, T* obase, int64_t o_st, int first_row, int Tq) {
   using V4 = typename Vec<T>::x4;
-  using V8 = typename Vec<T>::x8;
   constexpr int OSTR = D * 2;                  // unpadded rows; the 16-byte pieces are XOR-swizzled by row
   constexpr int PPR = D * 2 / 16;              // 16-byte pieces per row
+  constexpr int RPI = 64 / PPR;                // rows per 64-lane store instruction
+  const f32x2 iv = {inv, inv};
 #pragma unroll
   for (int db = 0; db < D / 32; ++db)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      V4 o4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o4[e] = (T)(oacc[db][4 * g + e] * inv);
+      const f32x2 a = f32x2{oacc[db][4 * g], oacc[db][4 * g + 1]} * iv;
+      const f32x2 c = f32x2{oacc[db][4 * g + 2], oacc[db][4 * g + 3]} * iv;
+      const V4 o4 = {(T)a[0], (T)a[1], (T)c[0], (T)c[1]};
       // piece db*4 + g of row r lands at piece (db*4 + g) ^ (r mod PPR): the 16 rows of a ds_write_b64 lane group
       // spread over the banks (2-way), and the row-contiguous read-back below is conflict-free
       *reinterpret_cast<V4*>(stage + r * OSTR + ((db * 4 + g) ^ (r & (PPR - 1))) * 16 + hh * 8) = o4;
     }
+  const int nrows = min(32, Tq - first_row);
+  const int ost2 = (int)o_st * 2;
+  const auto osrd = __builtin_amdgcn_make_buffer_rsrc((void*)(obase + (int64_t)first_row * o_st), (short)0,
+                                                      nrows > 0 ? (nrows - 1) * ost2 + OSTR : 0, 0x00020000);
+  const int lr = lane / PPR, pc = lane % PPR;
+  const uint32_t rx = (uint32_t)((pc ^ lr) * 16);   // row i*RPI + lr: (row mod PPR) = ((i*RPI) mod PPR) + lr
+  const int voff0 = lr * ost2 + pc * 16;
 #pragma unroll
-  for (int i = 0; i < 32 * PPR / 64; ++i) {
-    const int c = i * 64 + lane, row = c / PPR, pc = c % PPR;
-    const int qr = first_row + row * row_step;
-    const V8 v = *reinterpret_cast<const V8*>(stage + row * OSTR + (pc ^ (row & (PPR - 1))) * 16);
-    if (qr < Tq) *reinterpret_cast<V8*>(obase + (int64_t)qr * o_st + pc * 8) = v;
+  for (int i = 0; i < 32 / RPI; ++i) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(stage + (i * RPI + lr) * OSTR +
+                                                    (rx ^ (uint32_t)(((i * RPI) & (PPR - 1)) * 16)));
+    __builtin_amdgcn_raw_buffer_store_b128(v, osrd, voff0 + i * RPI * ost2, 0, 0);
   }
 }
 
@@ -281,15 +290,18 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
   const float* brow = en_any ? p.bias + b * p.bias_sb : nullptr;
 
   // Q as the B operand of S^T = K.Q^T: lane (r, hh) holds Q[qrow][16ks + 8hh .. +7]
+  // through a descriptor that ends at the wave's last row < Tq (rows past it read zeros): no per-row branch, the
+  // loads issue back to back
   V8 qf[D / 16];
+  {
+    const int qrows = min(32, Tq - q_row0);
+    const auto qsrd = __builtin_amdgcn_make_buffer_rsrc((void*)(qb + (int64_t)q_row0 * p.q_st), (short)0,
+                                                        qrows > 0 ? (int)((qrows - 1) * p.q_st * 2 + D * 2) : 0,
+                                                        0x00020000);
+    const int qv = r * (int)p.q_st * 2 + 16 * hh;
 #pragma unroll
-  for (int ks = 0; ks < D / 16; ++ks) {
-    if (qrow < Tq) {
-      qf[ks] = *reinterpret_cast<const V8*>(qb + qrow * p.q_st + 16 * ks + 8 * hh);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[ks][j] = (T)0.f;
-    }
+    for (int ks = 0; ks < D / 16; ++ks)
+      qf[ks] = __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(qsrd, qv + 32 * ks, 0, 0));
   }
 
   const int blk_last_q = min(qblk * BQ + BQ, Tq) - 1;
@@ -570,7 +582,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
 #endif
   // every wave passed the last tile's barrier: the stages are free for the O staging rows
   store_o_rows<T, D>(smem + wave * 32 * (D * 2), oacc, l > 0.f ? 1.f / l : 0.f, r, hh, lane,
-                     static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh, p.o_st, q_row0, 1, Tq);
+                     static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh, p.o_st, q_row0, Tq);
 }
 
 // one-wave-per-SIMD prefill (64 rows per wave, hand-ordered MFMA / softmax stream): prefill_x64_kernel
