@@ -523,7 +523,7 @@ class DecodeSession:
         # warm the allocator / kernels on a side stream, then restore the state it advanced
         snap = (self.tokens.clone(), self.pos.clone(), self.seq_lens.clone(), self.t.clone(), self.out.clone(),
                 None if self.seen is None else self.seen.clone())
-        with gemm_tune.pinned(), torch.cuda.stream(s):
+        with gemm_tune.pinned(decode=True), torch.cuda.stream(s):
             self._step_body()
         torch.cuda.current_stream(self.eng.device).wait_stream(s)
         self.tokens.copy_(snap[0]); self.pos.copy_(snap[1]); self.seq_lens.copy_(snap[2])
@@ -531,14 +531,14 @@ class DecodeSession:
         if self.seen is not None:
             self.seen.copy_(snap[5])
         self.graph = torch.cuda.CUDAGraph()
-        with gemm_tune.pinned(), torch.cuda.graph(self.graph):
+        with gemm_tune.pinned(decode=True), torch.cuda.graph(self.graph):
             self._step_body()
 
     def step(self, use_graph=True):
         if use_graph and self.graph is not None:
             self.graph.replay()
         else:
-            with gemm_tune.pinned():
+            with gemm_tune.pinned(decode=True):
                 self._step_body()
 
     def generated(self) -> torch.Tensor:

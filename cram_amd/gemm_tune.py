@@ -31,6 +31,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOLUTIONS = os.path.join(REPO, "data", "gemm_solutions.json")
 _installed = None
 _tried = None
+_decode_rows = frozenset()   # M values that have decode-step lines
+_scope = None                # "sweep" inside pinned(), "decode" inside pinned(decode=True)
 
 
 def _signature(N: int, K: int, M: int) -> str:
@@ -53,7 +55,7 @@ def validators_match(tuned: Dict[str, str]) -> bool:
 
 def install(m_values: Iterable[int], dtype: str = "BFloat16", path: str = SOLUTIONS) -> bool:
     """Pin the tuned solutions for every M in m_values; returns False (nothing pinned) on a different build."""
-    global _installed
+    global _installed, _decode_rows
     sol = load(path)
     if not validators_match(sol["validators"]):
         return False
@@ -79,25 +81,49 @@ def install(m_values: Iterable[int], dtype: str = "BFloat16", path: str = SOLUTI
         tun.tuning_enable(prev[1])
         os.unlink(fn)
     _installed = fn if ok else None
+    if ok:
+        _decode_rows = frozenset(int(k.split("x")[2]) for k in sol.get("decode_solutions", {}))
     return bool(ok)
 
 
 @contextlib.contextmanager
-def pinned():
+def pinned(decode: bool = False):
     """Use the pinned solutions for the GEMMs issued inside the block (TunableOp on, tuning off), then restore
-    the process's previous TunableOp state.  A no-op when nothing was pinned (other build, no GPU, A/B off)."""
+    the process's previous TunableOp state.  A no-op when nothing was pinned (other build, no GPU, A/B off).
+    decode=True: the decode step (its exact-M lines act); otherwise the sweep / prefill, where `shadowed(M)` tells
+    ops.linear to run a GEMM whose M has a decode line without TunableOp, so decode picks never touch the sweep."""
+    global _scope
     if not _tried:
         yield
         return
     tun = torch.cuda.tunable
-    prev = (tun.is_enabled(), tun.tuning_is_enabled())
+    prev = (tun.is_enabled(), tun.tuning_is_enabled(), _scope)
     tun.enable(True)
     tun.tuning_enable(False)
+    _scope = "decode" if decode else "sweep"
     try:
         yield
     finally:
         tun.enable(prev[0])
         tun.tuning_enable(prev[1])
+        _scope = prev[2]
+
+
+def shadowed(M: int) -> bool:
+    """True inside a sweep / prefill pinned() block for a row count that only decode steps may pin."""
+    return _scope == "sweep" and M in _decode_rows
+
+
+@contextlib.contextmanager
+def unpinned():
+    """TunableOp off for the GEMMs inside the block (restored after)."""
+    tun = torch.cuda.tunable
+    prev = tun.is_enabled()
+    tun.enable(False)
+    try:
+        yield
+    finally:
+        tun.enable(prev)
 
 
 def sweep_rows(lo: int = 8192, hi: int = 65536, step: int = 256) -> Tuple[int, ...]:

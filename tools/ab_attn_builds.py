@@ -41,10 +41,12 @@ def main():
     dev = torch.device("cuda:0")
     d = 128
     cases = []
-    for B, T, biased in [(33, 962, False), (1, 962, True), (1, 8300, False), (16, 8300, True)]:
+    # (B, T, biased, p0): p0 > 0 = the IE sweep's suffix call (T query rows after a p0-token shared prefix of keys)
+    for B, T, biased, p0 in [(33, 962, False, 0), (33, 937, False, 25), (1, 962, True, 0), (1, 8300, False, 0),
+                             (16, 8300, True, 0)]:
         g = torch.Generator(device=dev).manual_seed(B * T)
-        y = torch.randn(B, T, 48 * d, device=dev, generator=g).to(torch.bfloat16)
-        q = y[..., :32 * d].unflatten(-1, (32, d)).transpose(1, 2)
+        y = torch.randn(B, T + p0, 48 * d, device=dev, generator=g).to(torch.bfloat16)
+        q = y[:, p0:, :32 * d].unflatten(-1, (32, d)).transpose(1, 2)
         k = y[..., 32 * d:40 * d].unflatten(-1, (8, d)).transpose(1, 2)
         v = y[..., 40 * d:].unflatten(-1, (8, d)).transpose(1, 2)
         bias = enable = None
@@ -56,7 +58,7 @@ def main():
             enable = torch.ones(B, 32, dtype=torch.uint8, device=dev)
             W = T
         outs = [torch.empty(B, T, 32, d, device=dev, dtype=torch.bfloat16) for _ in libs]
-        cases.append(((B, T, biased), q, k, v, bias, enable, W, outs))
+        cases.append(((B, T, biased, p0), q, k, v, bias, enable, W, outs))
     for name, q, k, v, bias, enable, W, outs in cases:
         for lib, o in zip(libs, outs):
             call(lib, q, k, v, o, bias, enable, W)
@@ -77,8 +79,8 @@ def main():
                 torch.cuda.synchronize()
                 res[(i, name)].append(e0.elapsed_time(e1) / 10)
     for name, q, *_ in cases:
-        B, T, _b = name
-        fl, _ = ops.prefill_work(B, 32, 8, T, T, d, 0)
+        B, T, _b, p0 = name
+        fl, _ = ops.prefill_work(B, 32, 8, T, T + p0, d, p0)
         ms = [statistics.median(res[(i, name)]) for i in range(len(libs))]
         print(f"{str(name):22s} A {ms[0]:.3f} ms {fl / ms[0] / 1e9:6.0f} TF ({fl / ms[0] / 2.5e12:.3f})  "
               f"B {ms[1]:.3f} ms {fl / ms[1] / 1e9:6.0f} TF ({fl / ms[1] / 2.5e12:.3f})  B/A speed {ms[0] / ms[1]:.3f}x",
