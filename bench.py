@@ -78,6 +78,46 @@ def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, i
     return res
 
 
+def decode_leg_roofline(spec, phases, dtype):
+    """Roofline of the whole decode leg, from HIP events recorded inside it (engine.generate(phases=...)), summed
+    over the timed repeats:
+      prefill  MFMA-bound: algorithmic FLOPs of the packed prefill — per prompt of T tokens, every layer's
+               projections 2 * params * T (ModelSpec.layer_flops) + causal attention 4 * d * Hq * T(T+1)/2, and the
+               lm_head of the last row 2 * D * V — over the prefill's time, against the dense bf16 peak;
+      steps    HBM-bound: per greedy step, every weight once (L layers' projections + lm_head, the embedding is a
+               B-row gather) + every row's visible K and V (L * Hkv * d * 2 tensors * 2 B per key, the keys growing
+               by one per step) over the steps' time, against 8 TB/s (6.3 achievable)."""
+    import torch  # noqa: F401
+    L, D, V = spec.num_layers, spec.hidden, spec.vocab
+    esz = 2
+    p_layer = spec.hidden * (spec.q_size + 2 * spec.kv_size) + spec.q_size * spec.hidden + 3 * spec.hidden * spec.intermediate
+    w_bytes = (L * p_layer + V * D) * esz
+    kv_per_key = L * spec.num_kv_heads * spec.head_dim * 2 * esz
+    pf_flops = pf_ms = st_bytes = st_ms = cap_ms = 0.0
+    n_steps = 0
+    for ph in phases:
+        lens = ph["lens"]
+        for T in lens:
+            pf_flops += L * spec.layer_flops(T) + L * 4.0 * spec.head_dim * spec.num_heads * T * (T + 1) / 2 + 2.0 * D * V
+        pf_ms += ph["t0"].elapsed_time(ph["prefill"])
+        cap_ms += ph["prefill"].elapsed_time(ph["capture"])
+        st_ms += ph["capture"].elapsed_time(ph["steps"])
+        for t in range(1, ph["n_steps"] + 1):
+            st_bytes += w_bytes + kv_per_key * sum(T + t for T in lens)
+        n_steps += ph["n_steps"]
+    pf = pf_flops / (pf_ms * 1e-3) / 1e12
+    bw = st_bytes / (st_ms * 1e-3) / 1e9
+    return {"prefill": {"bound": "mfma", "achieved": round(pf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(pf / PEAK_BF16_TFLOPS, 4), "ms": round(pf_ms / len(phases), 2),
+                        "flops": pf_flops / len(phases)},
+            "steps": {"bound": "hbm", "achieved": round(bw, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                      "frac": round(bw / PEAK_HBM_GBS, 4), "ms": round(st_ms / len(phases), 2),
+                      "ms_per_step": round(st_ms / max(1, n_steps), 3), "bytes_per_step": st_bytes / max(1, n_steps),
+                      "weight_bytes_per_step": w_bytes},
+            "graph_capture_ms": round(cap_ms / len(phases), 2),
+            "note": "HIP events on the launch stream inside engine.generate, summed over the timed repeats"}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -277,10 +317,12 @@ def main():
         if world > 1:
             torch.distributed.barrier()
         reps = max(1, args.steps if args.config != 3 else 1)
+        phases = []
         td = time.perf_counter()
         for _ in range(reps):
+            phases.append({})
             eng.generate(prompts, ws, heads, max_new_tokens=args.decode_tokens, eos_ids=(), use_graph=True,
-                         stop_on_eos=False)
+                         stop_on_eos=False, phases=phases[-1])
         torch.cuda.synchronize()
         dt = torch.tensor([time.perf_counter() - td], device=dev, dtype=torch.float64)
         if world > 1:
@@ -293,6 +335,7 @@ def main():
                   "seconds": float(dt.item()), "repeats": reps,
                   "host_encode_ms_per_question": round(host_ms / B, 3),
                   "note": "packed varlen prefill + graph-replayed greedy steps, EOS ignored (random weights)"}
+        decode["leg_roofline"] = decode_leg_roofline(spec, phases, mdtype)
         decode["attention_roofline"] = decode_attention_roofline(eng, prompts, ws, heads, args.decode_tokens, dev)
         log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s (T mean {T_mean:.0f}); decode attention "
             f"{decode['attention_roofline']['achieved']:.0f} GB/s")

@@ -17,14 +17,14 @@ _c_int32_p = POINTER(ctypes.c_int32)
 _c_uint8_p = POINTER(ctypes.c_uint8)
 _c_float_p = POINTER(c_float)
 
-ABI_VERSION = 3   # CRAM_ABI_VERSION of include/cram_attn.h
+ABI_VERSION = 4   # CRAM_ABI_VERSION of include/cram_attn.h
 
 # name -> (restype, argtypes); the exact export list of include/cram_attn.h
 SIGNATURES = {
     "cram_strerror": (ctypes.c_char_p, [c_int]),
     "cram_abi_version": (c_int, []),
     "cram_set_knob": (c_int, [c_int, c_int]),
-    "cram_get_knob": (c_int, [c_int]),
+    "cram_get_knob": (c_int, [c_int, c_void_p]),
     "cram_attn_prefill": (c_int, [
         c_void_p, c_int64, c_int64, c_int64,
         c_void_p, c_int64, c_int64, c_int64,
@@ -67,6 +67,9 @@ SIGNATURES = {
     "cram_silu_mul": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_void_p]),
     "cram_gemm": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int,
                           c_void_p]),
+    "cram_gemm_splitk_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "cram_gemm_splitk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int,
+                                 c_int, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "cram_passage_weights": (c_int, [c_int] + [c_void_p] * 9),
 }
 
@@ -111,7 +114,12 @@ KNOB_DECODE_MFMA = 2       # CRAM_KNOB_DECODE_MFMA
 
 def set_knob(which: int, value: int) -> int:
     """Set a process-wide kernel-selection knob (-1 = automatic); returns the previous value."""
-    lib = load()
-    prev = lib.cram_get_knob(which)
-    check(lib.cram_set_knob(which, int(value)), "cram_set_knob")
+    prev = get_knob(which)
+    check(load().cram_set_knob(which, int(value)), "cram_set_knob")
     return prev
+
+
+def get_knob(which: int) -> int:
+    v = ctypes.c_int(0)
+    check(load().cram_get_knob(which, ctypes.byref(v)), "cram_get_knob")
+    return v.value

@@ -7,6 +7,7 @@ JIT cache) so the built ``.so`` travels with the repository snapshot.
 from __future__ import annotations
 
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -36,21 +37,104 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile ``libcram_attn.so`` for gfx950 if it is missing or stale."""
+    """Compile ``libcram_attn.so`` for gfx950 if it is missing or stale (one hipcc process per source, in
+    parallel, then one link)."""
     if not force and not needs_build():
         return LIB_PATH
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [
-        _hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-Wall", "-Wno-unused-function",
-        "-I", str(REPO_DIR / "include"),
-        *[str(s) for s in SOURCES], "-o", str(tmp),
-    ]
+    objdir = PKG_DIR / "build"
+    objdir.mkdir(exist_ok=True)
+    common = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+              "-I", str(REPO_DIR / "include")]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = objdir / (src.name + ".o")
+        # the attention library keeps its device assembly (same compile as the object) for the register audit
+        extra = ["-save-temps=obj"] if src.name == "cram_attn.hip" else []
+        cmd = common + extra + ["-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((subprocess.Popen(cmd), cmd))
+        objs.append(obj)
+    failed = [cmd for p, cmd in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+    bad = audit_x64(x64_asm_path().read_text())
+    if bad:
+        raise RuntimeError("prefill_x64_kernel register audit failed (the library is not installed): "
+                           + "; ".join(bad[:5]))
+    link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(tmp)]
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+        print(" ".join(link), file=sys.stderr)
+    subprocess.run(link, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
+
+
+def x64_asm_path() -> Path:
+    """Device assembly of cram_attn.hip saved by the last build (-save-temps=obj)."""
+    return PKG_DIR / "build" / f"cram_attn-hip-amdgcn-amd-amdhsa-{ARCH}.s"
+
+
+def kernel_body(asm: str, name: str) -> str:
+    m = re.search(r"^(_Z\w*" + name + r"\w*):", asm, re.M)
+    if not m:
+        raise RuntimeError(f"kernel {name} not found in the assembly")
+    return asm[m.end(): asm.find(".Lfunc_end", m.end())]
+
+
+def _sgprs(op: str) -> set:
+    m = re.fullmatch(r"s\[(\d+):(\d+)\]", op)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.fullmatch(r"s(\d+)", op)
+    return {int(m.group(1))} if m else set()
+
+
+_NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "s_barrier", "s_setprio", "s_endpgm")
+
+
+def audit_x64(asm: str) -> list:
+    """prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]) inside its inline asm;
+    hipcc knows nothing of that.  Returns the violations (empty = clean):
+      * any v_accvgpr_* / AGPR operand the COMPILER emitted (outside the kernel's ;;#ASMSTART..;;#ASMEND blocks);
+      * any scratch traffic in the kernel;
+      * an LDS-DMA whose descriptor SGPRs were written by a VALU op fewer than 5 wait states earlier (the kernel's
+        DMA pieces after the first of a tile carry no s_nop of their own)."""
+    body = kernel_body(asm, "prefill_x64_kernel")
+    bad = []
+    inside = False
+    for line in body.splitlines():
+        t = line.strip()
+        if t.startswith(";;#ASMSTART"):
+            inside = True
+        elif t.startswith(";;#ASMEND"):
+            inside = False
+        elif t and not t.startswith((";", ".")) and not inside and ("accvgpr" in t or re.search(r"\ba\[?\d", t)):
+            bad.append("compiler AGPR use: " + t)
+    if "scratch_" in body:
+        bad.append("scratch traffic in prefill_x64_kernel")
+    ins = [t.strip() for t in body.splitlines()]
+    ins = [t.replace(",", " ").split() for t in ins if t and not t.startswith((";", "."))]
+    n_dma = 0
+    for i, u in enumerate(ins):
+        if not (u[0].startswith("buffer_load") and u[-1] == "lds" and ins[i - 4] != ["s_nop", "4"]):
+            continue
+        n_dma += 1
+        srd = _sgprs(u[2])
+        if not srd:
+            bad.append("LDS-DMA without an SGPR descriptor: " + " ".join(u))
+            continue
+        states = 0
+        for w in reversed(ins[:i]):
+            if len(w) > 1 and not w[0].startswith(_NO_DST) and w[0].startswith(("s_", "v_")) and _sgprs(w[1]) & srd:
+                if w[0].startswith("v_") and states < 5:
+                    bad.append(f"descriptor hazard: {' '.join(w)} {states} states before {' '.join(u)}")
+                break
+            states += int(w[1]) + 1 if w[0] == "s_nop" else 1
+    if n_dma == 0:
+        bad.append("no LDS-DMA without its own s_nop found: the audit no longer matches the kernel")
+    return bad
 
 
 if __name__ == "__main__":

@@ -27,6 +27,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
+#include <mutex>
+
 #include <type_traits>
 
 #include "../../include/cram_attn.h"
@@ -1026,22 +1029,24 @@ __global__ __launch_bounds__(256) void answer_logits_kernel(const T* h, int64_t 
 // Process-wide kernel selection knobs (cram_set_knob): -1 = automatic.  The environment is read ONCE, at the
 // first query, as the initial value (CRAM_PREFILL_VARIANT = 3 | 8, CRAM_DECODE_U = 1 | 2 | 4); launches never
 // call getenv.  A knob changed after a hipGraph capture does not alter the captured launches.
-int g_knob[CRAM_KNOB_COUNT];
-bool g_knob_init = false;
+// Thread-safe: the environment is read under std::call_once and the values are atomics (a knob set from one
+// thread is seen by launches from any other; set knobs before launches whose choice they should affect).
+std::atomic<int> g_knob[CRAM_KNOB_COUNT];
+std::once_flag g_knob_once;
 inline void knobs_init() {
-  if (g_knob_init) return;
-  const char* e = getenv("CRAM_PREFILL_VARIANT");
-  g_knob[CRAM_KNOB_PREFILL_VARIANT] =
-      (e && (e[0] == '0' || e[0] == '3' || e[0] == '6' || e[0] == '7' || e[0] == '8')) ? e[0] - '0' : -1;
-  const char* eu = getenv("CRAM_DECODE_U");
-  g_knob[CRAM_KNOB_DECODE_U] = (eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1;
-  const char* em = getenv("CRAM_DECODE_MFMA");
-  g_knob[CRAM_KNOB_DECODE_MFMA] = (em && (em[0] == '0' || em[0] == '1')) ? em[0] - '0' : -1;
-  g_knob_init = true;
+  std::call_once(g_knob_once, [] {
+    const char* e = getenv("CRAM_PREFILL_VARIANT");
+    g_knob[CRAM_KNOB_PREFILL_VARIANT].store(
+        (e && (e[0] == '0' || e[0] == '3' || e[0] == '6' || e[0] == '7' || e[0] == '8')) ? e[0] - '0' : -1);
+    const char* eu = getenv("CRAM_DECODE_U");
+    g_knob[CRAM_KNOB_DECODE_U].store((eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1);
+    const char* em = getenv("CRAM_DECODE_MFMA");
+    g_knob[CRAM_KNOB_DECODE_MFMA].store((em && (em[0] == '0' || em[0] == '1')) ? em[0] - '0' : -1);
+  });
 }
 inline int knob(int k) {
   knobs_init();
-  return g_knob[k];
+  return g_knob[k].load(std::memory_order_relaxed);
 }
 
 inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -1182,13 +1187,14 @@ int cram_set_knob(int which, int value) {
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_MFMA && value != -1 && value != 0 && value != 1) return CRAM_ERR_INVALID_ARG;
-  g_knob[which] = value;
+  g_knob[which].store(value);
   return CRAM_OK;
 }
 
-int cram_get_knob(int which) {
-  if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
-  return knob(which);
+int cram_get_knob(int which, int* value) {
+  if (which < 0 || which >= CRAM_KNOB_COUNT || !value) return CRAM_ERR_INVALID_ARG;
+  *value = knob(which);
+  return CRAM_OK;
 }
 
 int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sb,

@@ -79,12 +79,16 @@ constexpr int IMG = 256 * ROWB;    // 32 KiB: one operand's image of one K-tile
 constexpr int STAGE = 2 * IMG;     // x image | y image
 constexpr int LDS_BYTES = 2 * STAGE;
 
+// internal epilogue of the split-K form: fp32 partial sums of one K range, combined by gemm_combine_kernel
+constexpr int EPI_PARTIAL = 100;
+
 struct GemmParams {
   const void* x; int64_t ldx;      // weights [N, K]
   const void* y; int64_t ldy;      // activations [M, K]
-  void* out; int64_t ldo;          // [M, N] (store) or [M, N / 2] (silu-mul)
+  void* out; int64_t ldo;          // [M, N] (store) or [M, N / 2] (silu-mul); EPI_PARTIAL: fp32 [splits][M][N]
   int M, N, K;
   int ntm, ntn, nblocks;
+  int splits, kts;                 // split-K: K ranges per output tile, K-tiles per range (K = splits * kts * BK)
 };
 
 __device__ __forceinline__ void barrier() {
@@ -118,7 +122,9 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[NA][NB], const Gem
     if (mb < p.M) {
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
-        if constexpr (EPI == CRAM_GEMM_STORE) {
+        if constexpr (EPI == EPI_PARTIAL) {
+          *reinterpret_cast<f32x4*>(static_cast<float*>(p.out) + (int64_t)mb * p.N + n + 16 * a) = acc[a][b];
+        } else if constexpr (EPI == CRAM_GEMM_STORE) {
           V4 v;
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = (T)acc[a][b][i];
@@ -146,38 +152,56 @@ template <typename T, int EPI>
 __global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
-  int tm, tn;
-  tile_of(p, blockIdx.x, tm, tn);
+  int tm, tn, ks = 0;
+  GemmParams pp = p;
+  if constexpr (EPI == EPI_PARTIAL) {
+    // split-K: bid = tile * splits + ks, so the workgroups of one K range (which read the same activation columns)
+    // share an XCD under round-robin dispatch when splits is a multiple of 8
+    const int tile = blockIdx.x / p.splits;
+    ks = blockIdx.x - tile * p.splits;
+    tm = tile % p.ntm;
+    tn = tile / p.ntm;
+    pp.out = static_cast<float*>(p.out) + (int64_t)ks * p.M * p.N;
+  } else {
+    tile_of(p, blockIdx.x, tm, tn);
+  }
   const int n0 = tn * BN, m0 = tm * BM;
+  const int k0 = ks * p.kts * BK, kc = p.kts * BK;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wx = wave >> 2, wy = wave & 3;
 
-  // buffer descriptors: x tile rows n0.., y tile rows m0.. (rows past M read as zeros)
-  const T* xb = static_cast<const T*>(p.x) + (int64_t)n0 * p.ldx;
-  const T* yb = static_cast<const T*>(p.y) + (int64_t)m0 * p.ldy;
+  // buffer descriptors: x tile rows n0.., y tile rows m0.., columns k0..k0+kc.  Every row offset lives in the
+  // per-lane voffset, the only part the range check covers: a y row at or past M has voffset >= the record count
+  // (ldy >= kc) and reads zeros; soffset carries only the K-tile offset inside the row.
+  const T* xb = static_cast<const T*>(p.x) + (int64_t)n0 * p.ldx + k0;
+  const T* yb = static_cast<const T*>(p.y) + (int64_t)m0 * p.ldy + k0;
   const int yrows = min(BM, p.M - m0);
-  const auto xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, (int)((BN - 1) * p.ldx * 2 + p.K * 2),
+  const auto xsrd = __builtin_amdgcn_make_buffer_rsrc((void*)xb, (short)0, (int)((BN - 1) * p.ldx * 2 + kc * 2),
                                                       0x00020000);
-  const auto ysrd = __builtin_amdgcn_make_buffer_rsrc((void*)yb, (short)0, (int)((yrows - 1) * p.ldy * 2 + p.K * 2),
+  const auto ysrd = __builtin_amdgcn_make_buffer_rsrc((void*)yb, (short)0, (int)((yrows - 1) * p.ldy * 2 + kc * 2),
                                                       0x00020000);
 
   // LDS-DMA: unit u, instruction i of this wave writes 8 rows (1 KiB) starting at tile row R(u, 2*wave + i);
   // lane L fetches row R + L/8, chunk (L%8) ^ swz(row)
   const int lr = lane >> 3, ls = lane & 7;
-  uint32_t vx[2], vy[2];
+  uint32_t vx[2], vy[2][2];
   int rx[2], ry[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int q = 2 * wave + i;
     rx[i] = q < 8 ? 8 * q : 128 + 8 * (q - 8);                // x_lo unit rows (x_hi: +64)
     ry[i] = (q >> 2) * 64 + 8 * (q & 3);                      // y_lo unit rows (y_hi: +32)
-    const int xr = rx[i] + lr, yr = ry[i] + lr;
+    const int xr = rx[i] + lr;
     vx[i] = (uint32_t)(xr * p.ldx * 2 + ((ls ^ ((xr >> 1) & 7)) * 16));
-    vy[i] = (uint32_t)(yr * p.ldy * 2 + ((ls ^ ((yr >> 1) & 7)) * 16));
+#pragma unroll
+    for (int hi = 0; hi < 2; ++hi) {
+      const int yr = ry[i] + 32 * hi + lr;                    // (yr >> 1) & 7 is the same for yr and yr + 32
+      vy[i][hi] = (uint32_t)(yr * p.ldy * 2 + ((ls ^ ((yr >> 1) & 7)) * 16));
+    }
   }
-  const int xhi_off = (int)(64 * p.ldx * 2), yhi_off = (int)(32 * p.ldy * 2);
+  const int xhi_off = (int)(64 * p.ldx * 2);
   char* const sbase = smem;
   auto stage_x = [&](int t, int hi) {          // x_lo (hi = 0) or x_hi (hi = 1) of K-tile t
     char* img = sbase + (t & 1) * STAGE;
@@ -190,8 +214,8 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
     char* img = sbase + (t & 1) * STAGE + IMG;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ysrd, (lds_void*)(img + (ry[i] + 32 * hi) * ROWB), 16, (int)vy[i],
-                                               t * ROWB + hi * yhi_off, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ysrd, (lds_void*)(img + (ry[i] + 32 * hi) * ROWB), 16,
+                                               (int)vy[i][hi], t * ROWB, 0, 0);
   };
 
   // fragment reads: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row tile, k chunk 4 ks + g
@@ -234,7 +258,7 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nt = p.K / BK;
+  const int nt = p.kts;
   // prologue: all of tile 0, and tile 1 except its x_hi unit (issued in tile 0's first phase)
   stage_x(0, 0); stage_y(0, 0); stage_y(0, 1); stage_x(0, 1);
   if (nt > 1) {
@@ -288,7 +312,57 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
   if (wx == 0) barrier();   // equal barrier counts for both halves
 
   // epilogue: lane (j, g) holds acc[a][b][i] = out[m0 + yrow0 + 16 b + j][n0 + xrow0 + 16 a + 4 g + i]
-  store_tile<T, EPI, 8, 4>(acc, p, m0 + yrow0 + fr, n0 + xrow0 + 4 * fg);
+  store_tile<T, EPI, 8, 4>(acc, pp, m0 + yrow0 + fr, n0 + xrow0 + 4 * fg);
+}
+
+// Split-K combine: out = epilogue(sum over the K ranges of the fp32 partials [splits][M][N], in range order — the
+// result does not depend on which workgroup finished first).  One thread per 8 output columns of one row.
+//   CRAM_GEMM_STORE         out[m, n] = rnd(sum + bias[n])            (bias optional: F.linear's addmm epilogue)
+//   CRAM_GEMM_SILU_MUL_CAT  x = [gate; up] rows (the checkpoint's own layout, F = N / 2):
+//                           out[m, f] = rnd(rnd(silu(rnd(g))) * rnd(u)), g = sum[m, f], u = sum[m, F + f]
+template <typename T, int EPI>
+__global__ __launch_bounds__(256) void gemm_combine_kernel(const float* __restrict__ part, int splits, int M, int N,
+                                                           const T* __restrict__ bias, T* __restrict__ out,
+                                                           int64_t ldo) {
+  using V4 = typename GVec<T>::x4;
+  const int nout = EPI == CRAM_GEMM_STORE ? N : N / 2;
+  const unsigned vpr = (unsigned)nout >> 3;
+  const unsigned gid = blockIdx.x * 256u + threadIdx.x;      // host guarantees M * vpr < 2^31
+  if (gid >= (unsigned)M * vpr) return;
+  const int m = (int)(gid / vpr);
+  const int c = (int)(gid % vpr) * 8;
+  const int64_t pstride = (int64_t)M * N;
+  const float* pr = part + (int64_t)m * N + c;
+  float a[8], u[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = u[j] = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(pr + s * pstride);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(pr + s * pstride + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { a[j] += a0[j]; a[4 + j] += a1[j]; }
+    if constexpr (EPI == CRAM_GEMM_SILU_MUL_CAT) {
+      const f32x4 u0 = *reinterpret_cast<const f32x4*>(pr + s * pstride + nout);
+      const f32x4 u1 = *reinterpret_cast<const f32x4*>(pr + s * pstride + nout + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { u[j] += u0[j]; u[4 + j] += u1[j]; }
+    }
+  }
+  V4 o0, o1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float r;
+    if constexpr (EPI == CRAM_GEMM_STORE) {
+      r = bias ? a[j] + (float)bias[c + j] : a[j];
+    } else {
+      const float g = rnd<T>(a[j]);
+      r = rnd<T>(g / (1.0f + expf(-g))) * rnd<T>(u[j]);
+    }
+    if (j < 4) o0[j] = (T)r; else o1[j - 4] = (T)r;
+  }
+  T* op = out + (int64_t)m * ldo + c;
+  *reinterpret_cast<V4*>(op) = o0;
+  *reinterpret_cast<V4*>(op + 4) = o1;
 }
 
 inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
@@ -309,6 +383,7 @@ extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx,
   GemmParams p;
   p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo;
   p.M = M; p.N = N; p.K = K;
+  p.splits = 1; p.kts = K / BK;
   p.ntm = (M + BM - 1) / BM;
   p.ntn = N / BN;
   const int64_t nb = (int64_t)p.ntm * p.ntn;
@@ -323,6 +398,58 @@ extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx,
   } else {
     if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
     else hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_SILU_MUL>), g, blk, 0, st, p);
+  }
+  return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}
+
+extern "C" size_t cram_gemm_splitk_workspace_size(int M, int N, int splits) {
+  if (M <= 0 || N <= 0 || splits <= 0) return 0;
+  return (size_t)splits * (size_t)M * (size_t)N * sizeof(float);
+}
+
+extern "C" int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo,
+                                int M, int N, int K, int splits, int epilogue, const void* bias, void* workspace,
+                                size_t ws_bytes, int dtype, cram_stream_t stream) {
+  if (!y || !x || !out || M <= 0 || N <= 0 || K <= 0 || splits <= 0) return CRAM_ERR_INVALID_ARG;
+  if (epilogue != CRAM_GEMM_STORE && epilogue != CRAM_GEMM_SILU_MUL_CAT) return CRAM_ERR_INVALID_ARG;
+  if (bias && epilogue != CRAM_GEMM_STORE) return CRAM_ERR_INVALID_ARG;
+  if (dtype != CRAM_DTYPE_BF16 && dtype != CRAM_DTYPE_F16) return CRAM_ERR_UNSUPPORTED;
+  if (N % BN != 0 || K % (BK * splits) != 0) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(y) || !al16(x) || !al16(out) || (ldy & 7) || (ldx & 7) || (ldo & 7)) return CRAM_ERR_ALIGNMENT;
+  if (bias && (reinterpret_cast<uintptr_t>(bias) & 15u)) return CRAM_ERR_ALIGNMENT;
+  const int nout = epilogue == CRAM_GEMM_STORE ? N : N / 2;
+  if (ldy < K || ldx < K || ldo < nout) return CRAM_ERR_INVALID_ARG;
+  if ((int64_t)BN * ldx * 2 >= (1ll << 31) || (int64_t)BM * ldy * 2 >= (1ll << 31)) return CRAM_ERR_UNSUPPORTED;
+  if (!workspace || ws_bytes < cram_gemm_splitk_workspace_size(M, N, splits)) return CRAM_ERR_WORKSPACE;
+  if ((reinterpret_cast<uintptr_t>(workspace) & 15u)) return CRAM_ERR_ALIGNMENT;
+  GemmParams p;
+  p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = workspace; p.ldo = N;
+  p.M = M; p.N = N; p.K = K;
+  p.splits = splits; p.kts = K / (BK * splits);
+  p.ntm = (M + BM - 1) / BM;
+  p.ntn = N / BN;
+  const int64_t nb = (int64_t)p.ntm * p.ntn * splits;
+  const int64_t nvec = (int64_t)M * (nout / 8);
+  if (nb > 0x7fffffff || nvec >= (1ll << 31)) return CRAM_ERR_INVALID_ARG;
+  p.nblocks = (int)nb;
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 gc((unsigned)((nvec + 255) / 256));
+  if (dtype == CRAM_DTYPE_BF16) {
+    hipLaunchKernelGGL((gemm_tn_kernel<__bf16, EPI_PARTIAL>), dim3(p.nblocks), dim3(512), 0, st, p);
+    if (epilogue == CRAM_GEMM_STORE)
+      hipLaunchKernelGGL((gemm_combine_kernel<__bf16, CRAM_GEMM_STORE>), gc, dim3(256), 0, st,
+                         (const float*)workspace, splits, M, N, (const __bf16*)bias, (__bf16*)out, ldo);
+    else
+      hipLaunchKernelGGL((gemm_combine_kernel<__bf16, CRAM_GEMM_SILU_MUL_CAT>), gc, dim3(256), 0, st,
+                         (const float*)workspace, splits, M, N, (const __bf16*)nullptr, (__bf16*)out, ldo);
+  } else {
+    hipLaunchKernelGGL((gemm_tn_kernel<_Float16, EPI_PARTIAL>), dim3(p.nblocks), dim3(512), 0, st, p);
+    if (epilogue == CRAM_GEMM_STORE)
+      hipLaunchKernelGGL((gemm_combine_kernel<_Float16, CRAM_GEMM_STORE>), gc, dim3(256), 0, st,
+                         (const float*)workspace, splits, M, N, (const _Float16*)bias, (_Float16*)out, ldo);
+    else
+      hipLaunchKernelGGL((gemm_combine_kernel<_Float16, CRAM_GEMM_SILU_MUL_CAT>), gc, dim3(256), 0, st,
+                         (const float*)workspace, splits, M, N, (const _Float16*)nullptr, (_Float16*)out, ldo);
   }
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
 }

@@ -12,15 +12,19 @@ data-path collective is needed; at the end one `all_gather_into_tensor` (backend
 grid [Nq, L, H] on every rank.
 
 Checkpoint / resume (find_best_heads.py:30-40,53-58 resumes by skipping questions
-already on file): with `shard_dir`, every rank appends one JSON line per finished
-(question, layer) to its own file `rank{r}.jsonl` (append-only, fsync'd per work
-item); a restarted run — any world size — reads every shard file, skips the units
-already there and fills them from disk.  Decode is replica-only (question-sharded,
+already on file, by index into a fixed input file): with `shard_dir`, every rank
+appends one JSON line per finished (question, layer) to its own file
+`rank{r}.jsonl` (append-only, fsync'd per work item), keyed by the question's
+identity (a hash of question, passages, scores and wrong answer) and a run
+fingerprint (model, shapes, logit convention); a restarted run — any world size,
+any order or subset of questions — reads every shard file, skips the units whose
+(identity, layer) is already there and fills them from disk.  Decode is replica-only (question-sharded,
 no collective).
 """
 from __future__ import annotations
 
 import glob
+import hashlib
 import heapq
 import json
 import os
@@ -130,10 +134,17 @@ def plan(costs: Sequence[float], num_layers: int, world: int) -> List[List[WorkI
     return [[(i, list(snake[r])) for i in range(nq)] if snake[r] else [] for r in range(world)]
 
 
-def read_shards(shard_dir: str, num_heads: int) -> Dict[Tuple[int, int], List[float]]:
-    """{(question, layer): IE row} from every rank's append-only file; a torn last line (a killed writer) is
-    ignored, a later line for the same unit wins."""
-    done: Dict[Tuple[int, int], List[float]] = {}
+def unit_key(*parts) -> str:
+    """Identity of one question's units for checkpoint files: a hash of everything that determines its IE rows
+    (question, passages, scores, wrong answer).  Resume matches on it, never on the position in the list."""
+    return hashlib.sha256(json.dumps(parts, ensure_ascii=False, sort_keys=True).encode("utf-8")).hexdigest()[:24]
+
+
+def read_shards(shard_dir: str, num_heads: int, run: str = "") -> Dict[Tuple[str, int], List[float]]:
+    """{(question key, layer): IE row} from every rank's append-only file, restricted to records of this run
+    fingerprint (model, layer / head counts, logit convention); a torn line (a killed writer) is ignored, a later
+    line for the same unit wins."""
+    done: Dict[Tuple[str, int], List[float]] = {}
     for fn in sorted(glob.glob(os.path.join(shard_dir, "rank*.jsonl"))):
         with open(fn, encoding="utf-8") as f:
             for line in f:
@@ -141,26 +152,36 @@ def read_shards(shard_dir: str, num_heads: int) -> Dict[Tuple[int, int], List[fl
                     rec = json.loads(line)
                 except ValueError:
                     continue
-                if isinstance(rec, dict) and len(rec.get("ie", ())) == num_heads:
-                    done[(int(rec["q"]), int(rec["layer"]))] = [float(x) for x in rec["ie"]]
+                if (isinstance(rec, dict) and isinstance(rec.get("key"), str) and rec.get("run", "") == run
+                        and len(rec.get("ie", ())) == num_heads):
+                    done[(rec["key"], int(rec["layer"]))] = [float(x) for x in rec["ie"]]
     return done
 
 
 class ShardWriter:
-    """Append-only per-rank checkpoint file: one line {"q", "layer", "ie"} per finished (question, layer)."""
+    """Append-only per-rank checkpoint file: one line {"key", "run", "layer", "ie", "q"} per finished (question,
+    layer); "q" (the position in this run's list) is informational only."""
 
-    def __init__(self, shard_dir: str, rank: int, qid: Optional[Sequence] = None):
+    def __init__(self, shard_dir: str, rank: int, keys: Sequence[str], run: str = ""):
         os.makedirs(shard_dir, exist_ok=True)
         self.path = os.path.join(shard_dir, f"rank{rank}.jsonl")
-        self.qid = qid
+        self.keys = list(keys)
+        self.run = run
+        # a writer killed mid-line left a fragment without its newline: end it, so the next record starts its own
+        # line (the fragment stays an unparsable line that read_shards skips)
+        if os.path.exists(self.path) and os.path.getsize(self.path) > 0:
+            with open(self.path, "rb+") as f:
+                f.seek(-1, os.SEEK_END)
+                if f.read(1) != b"\n":
+                    f.write(b"\n")
+                    f.flush()
+                    os.fsync(f.fileno())
 
     def write(self, q: int, layers: Sequence[int], ie_rows) -> None:
         rows = ie_rows.tolist() if hasattr(ie_rows, "tolist") else ie_rows
         lines = []
         for l, row in zip(layers, rows):
-            rec = {"q": int(q), "layer": int(l), "ie": [float(x) for x in row]}
-            if self.qid is not None:
-                rec["id"] = self.qid[q]
+            rec = {"key": self.keys[q], "run": self.run, "layer": int(l), "ie": [float(x) for x in row], "q": int(q)}
             lines.append(json.dumps(rec) + "\n")
         with open(self.path, "a", encoding="utf-8") as f:
             f.write("".join(lines))
@@ -170,21 +191,26 @@ class ShardWriter:
 
 def sweep_sharded(fn: Callable[[int, List[int]], torch.Tensor], n_questions: int, costs: Sequence[float],
                   num_layers: int, num_heads: int, device, shard_dir: Optional[str] = None, group=None,
-                  qid: Optional[Sequence] = None, log: Optional[Callable[[str], None]] = None) -> torch.Tensor:
+                  keys: Optional[Sequence[str]] = None, run: str = "",
+                  log: Optional[Callable[[str], None]] = None) -> torch.Tensor:
     """IE [Nq, L, H] (fp32, on `device`, identical on every rank) of n_questions questions.
 
     fn(i, layers) -> IE rows [len(layers), H] of question i (cram_amd.sweep.ie_question(..., layers=layers)).
-    Work is planned by `plan`; with shard_dir, finished units are checkpointed per work item and a restarted
-    run skips every unit already on disk.  The rows computed in this run travel in ONE all-gather."""
+    Work is planned by `plan`; with shard_dir, finished units are checkpointed per work item under the question's
+    identity keys[i] (unit_key) and the run fingerprint `run`, and a restarted run — any world size, any order or
+    subset of questions — reuses exactly the units whose (key, layer) is on disk for the same run.  The rows
+    computed in this run travel in ONE all-gather."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     world = dist.get_world_size(group) if dist.is_initialized() else 1
-    done = read_shards(shard_dir, num_heads) if shard_dir else {}
+    if shard_dir and (keys is None or len(keys) != n_questions):
+        raise ValueError("checkpointing needs one identity key per question (cram_amd.dist.unit_key)")
+    done = read_shards(shard_dir, num_heads, run) if shard_dir else {}
     if shard_dir and world > 1:
         dist.barrier(group)                   # every rank has read the same files before anyone appends
-    writer = ShardWriter(shard_dir, rank, qid) if shard_dir else None
+    writer = ShardWriter(shard_dir, rank, keys, run) if shard_dir else None
     rows, ids = [], []
     for q, layers in plan(costs, num_layers, world)[rank]:
-        todo = [l for l in layers if (q, l) not in done]
+        todo = [l for l in layers if not shard_dir or (keys[q], l) not in done]
         if not todo:
             continue
         ie = fn(q, todo).to(device, torch.float32)
@@ -196,7 +222,10 @@ def sweep_sharded(fn: Callable[[int, List[int]], torch.Tensor], n_questions: int
             log(f"[rank {rank}] question {q}: {len(todo)} layers")
     local = torch.cat(rows) if rows else torch.zeros((0, num_heads), dtype=torch.float32, device=device)
     out = gather_rows(local, torch.tensor(ids, dtype=torch.int64), n_questions * num_layers, group)
-    for (q, l), row in done.items():
-        if q < n_questions and l < num_layers:
-            out[q * num_layers + l] = torch.tensor(row, dtype=torch.float32, device=out.device)
+    if shard_dir:
+        for q in range(n_questions):
+            for l in range(num_layers):
+                row = done.get((keys[q], l))
+                if row is not None:
+                    out[q * num_layers + l] = torch.tensor(row, dtype=torch.float32, device=out.device)
     return out.view(n_questions, num_layers, num_heads)

@@ -336,7 +336,7 @@ class CrAMEngine:
     def generate(self, prompts: Sequence[torch.Tensor], weights16: Sequence[torch.Tensor], layers_to_heads: dict,
                  max_new_tokens: int = 100, eos_ids: Sequence[int] = (), bad_token_ids: Sequence[int] = (),
                  use_graph: bool = True, stop_on_eos: bool = True,
-                 repetition_penalty: float = 1.0) -> List[List[int]]:
+                 repetition_penalty: float = 1.0, phases: Optional[dict] = None) -> List[List[int]]:
         """Greedy decode of several prompts at once (per-row lengths, per-row credibility bias).
 
         Returns the generated ids of every prompt, truncated after its first EOS
@@ -344,20 +344,40 @@ class CrAMEngine:
         one-at-a-time generation as in re_weighting.py:127-132).  repetition_penalty != 1 applies transformers'
         RepetitionPenaltyLogitsProcessor (the checkpoint's generation_config, e.g. Qwen chat models ship 1.05)
         over each row's prompt and generated ids.
+        phases: a dict that receives HIP events on the launch stream around the packed prefill, the step-graph
+        capture and the decode steps ("t0", "prefill", "capture", "steps") plus the step count and the session's
+        row lengths, for timing the leg's phases without a host sync inside it.
         """
+        ev = (lambda: torch.cuda.Event(enable_timing=True)) if phases is not None else None
+        if ev is not None:
+            phases["t0"] = ev()
+            phases["t0"].record()
         sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids,
                              repetition_penalty)
         sess.prefill()
+        if ev is not None:
+            phases["prefill"] = ev()
+            phases["prefill"].record()
         steps = max_new_tokens - 1
         if use_graph and steps > 0:
             sess.capture()
+        if ev is not None:
+            phases["capture"] = ev()
+            phases["capture"].record()
         eos = torch.tensor(list(eos_ids) or [-1], device=self.device)
+        n_steps = 0
         for t in range(steps):
             sess.step(use_graph)
+            n_steps += 1
             # every 8 steps: stop once every row has produced an EOS (one host sync per check)
             if stop_on_eos and eos_ids and (t % 8 == 7 or t == steps - 1):
                 if bool(torch.isin(sess.generated(), eos).any(1).all()):
                     break
+        if ev is not None:
+            phases["steps"] = ev()
+            phases["steps"].record()
+            phases["n_steps"] = n_steps
+            phases["lens"] = list(sess.lens)
         out = []
         gen = sess.generated().cpu().tolist()
         for row in gen:

@@ -351,6 +351,7 @@ def silu_mul(gu: torch.Tensor, F: int, out: Optional[torch.Tensor] = None) -> to
 
 GEMM_STORE = 0      # CRAM_GEMM_STORE
 GEMM_SILU_MUL = 1   # CRAM_GEMM_SILU_MUL
+GEMM_SILU_MUL_CAT = 2   # CRAM_GEMM_SILU_MUL_CAT
 
 
 def interleave_gate_up(wgu: torch.Tensor, F: int) -> torch.Tensor:
@@ -382,6 +383,45 @@ def gemm(x: torch.Tensor, w: torch.Tensor, epilogue: int = GEMM_STORE, out: Opti
     code = _lib.load().cram_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(), o2.stride(0),
                                  M, N, K, int(epilogue), _dt(x), _stream(x.device))
     _lib.check(code, "cram_gemm")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(x.device))
+    return out
+
+
+def gemm_splitk_workspace_bytes(M: int, N: int, splits: int) -> int:
+    return int(_lib.load().cram_gemm_splitk_workspace_size(int(M), int(N), int(splits)))
+
+
+def gemm_splitk(x: torch.Tensor, w: torch.Tensor, splits: int, epilogue: int = GEMM_STORE,
+                bias: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, name: str = "cram_gemm_splitk") -> torch.Tensor:
+    """x [..., K] @ w[N, K]^T (+ bias) with K cut into `splits` ranges (cram_gemm_splitk: the decode step's skinny
+    projections); GEMM_SILU_MUL_CAT takes the checkpoint's [gate; up] weight and returns the MLP activation
+    [..., N/2].  workspace: a uint8 device tensor of >= gemm_splitk_workspace_bytes(M, N, splits) (allocated here
+    when None; pass one for hipGraph capture)."""
+    _dt(x)
+    if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("w must be a [N, K] row-major weight of x's dtype")
+    x2 = _rows2d(x, "x")
+    M, K = x2.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"K mismatch: x {K}, w {w.shape[1]}")
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous [N] tensor of x's dtype")
+    nout = N if epilogue == GEMM_STORE else N // 2
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (nout,), dtype=x.dtype, device=x.device)
+    o2 = _rows2d(out, "out")
+    need = gemm_splitk_workspace_bytes(M, N, splits)
+    if workspace is None:
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    ev = TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout), x.device) if TIMER.enabled else None
+    code = _lib.load().cram_gemm_splitk(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
+                                        o2.stride(0), M, N, K, int(splits), int(epilogue),
+                                        None if bias is None else bias.data_ptr(), workspace.data_ptr(),
+                                        workspace.numel(), _dt(x), _stream(x.device))
+    _lib.check(code, "cram_gemm_splitk")
     if ev is not None:
         ev.record(torch.cuda.current_stream(x.device))
     return out

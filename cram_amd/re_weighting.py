@@ -260,8 +260,13 @@ class Find_Best_Heads(Re_Weighting_Strategy):
                  for q, p, a in zip(questions, paras_list, wrong_answers)]
         fn = lambda i, layers: self.cal_logits_tensor(questions[i], paras_list[i], scores_list[i], "",
                                                       wrong_answers[i], round_logits, layers=layers)
+        keys = [_dist.unit_key(q, list(p), [float(x) for x in s], a)
+                for q, p, s, a in zip(questions, paras_list, scores_list, wrong_answers)]
+        run = (f"{self.model_name}|L{self.model_num_hidden_layers}|H{self.model_num_attention_heads}|"
+               f"{str(self.model.dtype).replace('torch.', '')}|round_logits={bool(round_logits)}")
         return _dist.sweep_sharded(fn, len(questions), costs, self.model_num_hidden_layers,
-                                   self.model_num_attention_heads, self.device, shard_dir=shard_dir, group=group)
+                                   self.model_num_attention_heads, self.device, shard_dir=shard_dir, group=group,
+                                   keys=keys, run=run)
 
     def cal_logits(self, question: str = "", paras: list = (), scores: list = (), right_answer: str = "",
                    wrong_answer: str = "my name is") -> list:

@@ -48,7 +48,8 @@ extern "C" {
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
 
-#define CRAM_ABI_VERSION 3        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs */
+#define CRAM_ABI_VERSION 4        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
+                                     4: cram_get_knob(which, *value), decode projection GEMM */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -61,8 +62,8 @@ int cram_abi_version(void);
 /*
  * Process-wide kernel-selection knobs (A/B runs and tests; the product default is automatic = -1).
  * The initial values are read once from the environment (CRAM_PREFILL_VARIANT, CRAM_DECODE_U, CRAM_DECODE_MFMA) at
- * the first query; no launch reads the environment.  Not synchronised: set knobs before launching from other
- * threads.
+ * the first query (once per process, thread-safe); no launch reads the environment.  Knob values are atomics:
+ * a value set from one thread is seen by launches issued afterwards from any thread.
  *   CRAM_KNOB_PREFILL_VARIANT  -1 = automatic: 64-key tiles, 4 waves, except GQA-7 groups with sequences <= 2048
  *                              (7-wave workgroups) and bf16 GQA groups of 4k with >= 4096 query rows (variant 6);
  *                              0 = always 4 waves; 3 = 32-key tiles; 8 = 8-wave workgroups;
@@ -70,14 +71,16 @@ int cram_abi_version(void);
  *                              (bf16, d = 128, GQA groups of 4k; otherwise as 0)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
- * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob returns the value.
+ * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob stores the value in
+ * *value and returns CRAM_OK, or CRAM_ERR_INVALID_ARG for an unknown knob / null pointer (ABI 4: the value -1,
+ * "automatic", is never an error code).
  */
 #define CRAM_KNOB_PREFILL_VARIANT 0
 #define CRAM_KNOB_DECODE_U 1
 #define CRAM_KNOB_DECODE_MFMA 2
 #define CRAM_KNOB_COUNT 3
 int cram_set_knob(int which, int value);
-int cram_get_knob(int which);
+int cram_get_knob(int which, int* value);
 
 /*
  * Prefill / multi-token attention (replaces the hooked SDPA call for
@@ -185,8 +188,25 @@ int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows
  */
 #define CRAM_GEMM_STORE 0
 #define CRAM_GEMM_SILU_MUL 1
+#define CRAM_GEMM_SILU_MUL_CAT 2
 int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N, int K,
               int epilogue, int dtype, cram_stream_t stream);
+
+/*
+ * Split-K form of the same GEMM for the decode step's projections (few activation rows, M = the batch: 256 at
+ * config 2, 16 at config 5; re_weighting.py:127-132 runs them inside generate, one token per step).  K is cut into
+ * `splits` equal ranges (K % (64 * splits) == 0), every (256 x 256 output tile, K range) is one workgroup writing
+ * fp32 partial sums to the caller's workspace [splits][M][N] (cram_gemm_splitk_workspace_size bytes, 16-B
+ * aligned), and a combine pass adds the ranges in range order (deterministic: no atomics) and applies
+ *   CRAM_GEMM_STORE         out [M][N] (ldo) = rnd(sum + bias[n])   (bias [N] or NULL: nn.Linear with bias)
+ *   CRAM_GEMM_SILU_MUL_CAT  x = [gate; up] rows as the checkpoint stores them ([2F][K], F = N / 2);
+ *                           out [M][F] (ldo) = rnd(rnd(silu(rnd(g))) * rnd(u)), cram_silu_mul's arithmetic
+ * Same requirements as cram_gemm plus ldo % 8 == 0; returns CRAM_ERR_WORKSPACE for a missing / short workspace.
+ */
+size_t cram_gemm_splitk_workspace_size(int M, int N, int splits);
+int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N,
+                     int K, int splits, int epilogue, const void* bias, void* workspace, size_t ws_bytes, int dtype,
+                     cram_stream_t stream);
 
 /*
  * Host-side prompt -> credibility weights (cram_spans.cpp; no device, no stream), batched over B prompts.

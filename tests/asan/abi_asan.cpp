@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "cram_attn.h"
@@ -111,12 +112,47 @@ static void validation_paths() {
   EXPECT(cram_set_knob(-1, 0) == CRAM_ERR_INVALID_ARG);
   EXPECT(cram_set_knob(CRAM_KNOB_PREFILL_VARIANT, 5) == CRAM_ERR_INVALID_ARG);
   EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, 3) == CRAM_ERR_INVALID_ARG);
-  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, 2) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_U) == 2);
-  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, -1) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_U) == -1);
-  EXPECT(cram_get_knob(7) == CRAM_ERR_INVALID_ARG);
+  int kv = 0;
+  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, 2) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_U, &kv) == CRAM_OK &&
+         kv == 2);
+  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, -1) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_U, &kv) == CRAM_OK &&
+         kv == -1);
+  kv = 5;
+  EXPECT(cram_get_knob(7, &kv) == CRAM_ERR_INVALID_ARG && kv == 5);
+  EXPECT(cram_get_knob(CRAM_KNOB_DECODE_U, nullptr) == CRAM_ERR_INVALID_ARG);
   EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, 2) == CRAM_ERR_INVALID_ARG);
-  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, 0) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_MFMA) == 0);
+  EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, 0) == CRAM_OK && cram_get_knob(CRAM_KNOB_DECODE_MFMA, &kv) == CRAM_OK &&
+         kv == 0);
   EXPECT(cram_set_knob(CRAM_KNOB_DECODE_MFMA, -1) == CRAM_OK);
+  // knobs from several host threads at once (std::call_once + atomics): no data race for the sanitizer to see
+  {
+    std::vector<std::thread> th;
+    for (int i = 0; i < 8; ++i)
+      th.emplace_back([i] {
+        int v = 0;
+        for (int r = 0; r < 1000; ++r) {
+          cram_set_knob(CRAM_KNOB_DECODE_U, (i & 1) ? 1 : 2);
+          cram_get_knob(CRAM_KNOB_DECODE_U, &v);
+        }
+      });
+    for (auto& t : th) t.join();
+    EXPECT(cram_set_knob(CRAM_KNOB_DECODE_U, -1) == CRAM_OK);
+  }
+  // split-K GEMM argument validation
+  const size_t ws = cram_gemm_splitk_workspace_size(16, 512, 4);
+  EXPECT(ws == 4u * 16u * 512u * 4u && cram_gemm_splitk_workspace_size(0, 512, 4) == 0);
+  EXPECT(cram_gemm_splitk(f, 512, f, 512, f, 512, 16, 512, 512, 3, CRAM_GEMM_STORE, nullptr, f, ws, 0, nullptr) ==
+         CRAM_ERR_UNSUPPORTED);
+  EXPECT(cram_gemm_splitk(f, 512, f, 512, f, 512, 16, 512, 512, 4, CRAM_GEMM_SILU_MUL, nullptr, f, ws, 0,
+                          nullptr) == CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_gemm_splitk(f, 512, f, 512, f, 512, 16, 512, 512, 4, CRAM_GEMM_SILU_MUL_CAT, f, f, ws, 0, nullptr) ==
+         CRAM_ERR_INVALID_ARG);
+  EXPECT(cram_gemm_splitk(f, 512, f, 512, f, 512, 16, 512, 512, 4, CRAM_GEMM_STORE, nullptr, nullptr, ws, 0,
+                          nullptr) == CRAM_ERR_WORKSPACE);
+  EXPECT(cram_gemm_splitk(f, 512, f, 512, f, 512, 16, 512, 512, 4, CRAM_GEMM_STORE, nullptr, f, ws - 1, 0,
+                          nullptr) == CRAM_ERR_WORKSPACE);
+  EXPECT(cram_gemm_splitk(f, 512, f, 512, f, 512, 16, 512, 512, 4, CRAM_GEMM_STORE, nullptr, f, ws, 7, nullptr) ==
+         CRAM_ERR_UNSUPPORTED);
 }
 
 static uint16_t f16_bits(float x) {

@@ -30,7 +30,7 @@ def test_library_builds_loads_and_exports_every_symbol():
         assert hasattr(lib, n), n
     assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
     L = _lib.load()
-    assert L.cram_abi_version() == _lib.ABI_VERSION == 3
+    assert L.cram_abi_version() == _lib.ABI_VERSION == 4
     assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0
@@ -65,6 +65,15 @@ def test_argument_validation_without_gpu():
     assert L.cram_gemm(fake, 68, fake, 64, fake, 256, 1, 256, 64, 0, 0, None) == -3
     assert L.cram_gemm(fake, 64, fake, 64, fake, 256, 1, 256, 64, 2, 0, None) == -1
     assert L.cram_gemm(fake, 64, fake, 64, fake, 128, 1, 512, 64, 0, 0, None) == -1
+    # split-K GEMM: K % (64 * splits), epilogue, bias only with STORE, workspace presence and size
+    ws = L.cram_gemm_splitk_workspace_size(16, 512, 4)
+    assert ws == 4 * 16 * 512 * 4
+    assert L.cram_gemm_splitk(fake, 512, fake, 512, fake, 512, 16, 512, 512, 3, 0, None, fake, ws, 0, None) == -2
+    assert L.cram_gemm_splitk(fake, 512, fake, 512, fake, 512, 16, 512, 512, 4, 1, None, fake, ws, 0, None) == -1
+    assert L.cram_gemm_splitk(fake, 512, fake, 512, fake, 512, 16, 512, 512, 4, 2, fake, fake, ws, 0, None) == -1
+    assert L.cram_gemm_splitk(fake, 512, fake, 512, fake, 512, 16, 512, 512, 4, 0, None, None, ws, 0, None) == -5
+    assert L.cram_gemm_splitk(fake, 512, fake, 512, fake, 512, 16, 512, 512, 4, 0, None, fake, ws - 1, 0, None) == -5
+    assert L.cram_gemm_splitk(fake, 512, fake, 512, fake, 260, 16, 512, 512, 4, 2, None, fake, ws, 0, None) == -3
 
 
 def test_kernel_knobs_latch_without_gpu():
@@ -73,11 +82,16 @@ def test_kernel_knobs_latch_without_gpu():
     L = _lib.load()
     prev = _lib.set_knob(_lib.KNOB_DECODE_U, 2)
     try:
-        assert L.cram_get_knob(_lib.KNOB_DECODE_U) == 2
+        assert _lib.get_knob(_lib.KNOB_DECODE_U) == 2
         os.environ["CRAM_DECODE_U"] = "4"            # the environment is not re-read after the first query
-        assert L.cram_get_knob(_lib.KNOB_DECODE_U) == 2
+        assert _lib.get_knob(_lib.KNOB_DECODE_U) == 2
         with pytest.raises(RuntimeError):
             _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, 5)
+        # an unknown knob is an error code distinct from every knob value (-1 = automatic is a value)
+        v = ctypes.c_int(123)
+        assert L.cram_get_knob(99, ctypes.byref(v)) == -1 and v.value == 123
+        assert L.cram_get_knob(_lib.KNOB_DECODE_U, None) == -1
+        assert _lib.set_knob(_lib.KNOB_DECODE_MFMA, -1) in (-1, 0, 1) and _lib.get_knob(_lib.KNOB_DECODE_MFMA) == -1
     finally:
         os.environ.pop("CRAM_DECODE_U", None)
         _lib.set_knob(_lib.KNOB_DECODE_U, prev)

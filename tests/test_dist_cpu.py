@@ -56,14 +56,49 @@ def test_gather_rows_single_process():
     assert torch.equal(out[3], local[0]) and torch.equal(out[0], local[1]) and out[1].abs().sum() == 0
 
 
+KEYS = ["qa", "qb", "qc"]
+
+
 def test_shard_files_tolerate_a_torn_line(tmp_path):
-    w = cdist.ShardWriter(str(tmp_path), 0)
+    w = cdist.ShardWriter(str(tmp_path), 0, KEYS)
     w.write(2, [0, 3], torch.tensor([[1.5, -2.0], [0.25, 3.0]]))
     with open(tmp_path / "rank0.jsonl", "a") as f:
-        f.write('{"q": 2, "layer": 1, "ie": [0.1')       # a writer killed mid-line
-    cdist.ShardWriter(str(tmp_path), 1).write(1, [1], [[7.0, 8.0]])
+        f.write('{"key": "qc", "run": "", "layer": 1, "ie": [0.1')       # a writer killed mid-line
+    cdist.ShardWriter(str(tmp_path), 1, KEYS).write(1, [1], [[7.0, 8.0]])
     done = cdist.read_shards(str(tmp_path), 2)
-    assert done == {(2, 0): [1.5, -2.0], (2, 3): [0.25, 3.0], (1, 1): [7.0, 8.0]}
+    assert done == {("qc", 0): [1.5, -2.0], ("qc", 3): [0.25, 3.0], ("qb", 1): [7.0, 8.0]}
+    # the SAME rank restarts after the torn line: its next record must not be glued onto the fragment
+    cdist.ShardWriter(str(tmp_path), 0, KEYS).write(0, [2], [[4.0, 5.0]])
+    done = cdist.read_shards(str(tmp_path), 2)
+    assert done[("qa", 2)] == [4.0, 5.0] and len(done) == 4
+
+
+def test_resume_matches_question_identity_not_position(tmp_path):
+    """A restart over a reordered / different question list reuses only the units of the same questions, and only
+    from the same run fingerprint (find_best_heads.py:30-40 resumes by index into a fixed file; here lists vary)."""
+    d = str(tmp_path)
+    calls = []
+
+    def fn(i, layers, tag):
+        calls.append((tag, i, tuple(layers)))
+        return torch.tensor([[float(ord(tag[0])) * 100 + i * 10 + l, -1.0] for l in layers])
+
+    first = ["qa", "qb", "qc"]
+    out1 = cdist.sweep_sharded(lambda i, ls: fn(i, ls, first[i]), 3, [1.0, 1.0, 1.0], 2, 2, torch.device("cpu"),
+                               shard_dir=d, keys=first, run="m1")
+    assert len(calls) == 3
+    calls.clear()
+    second = ["qc", "qx", "qa"]                  # reordered, one new question
+    out2 = cdist.sweep_sharded(lambda i, ls: fn(i, ls, second[i]), 3, [1.0, 1.0, 1.0], 2, 2, torch.device("cpu"),
+                               shard_dir=d, keys=second, run="m1")
+    assert calls == [("qx", 1, (0, 1))]          # only the new question is computed
+    assert torch.equal(out2[0], out1[2]) and torch.equal(out2[2], out1[0])
+    calls.clear()
+    cdist.sweep_sharded(lambda i, ls: fn(i, ls, second[i]), 3, [1.0, 1.0, 1.0], 2, 2, torch.device("cpu"),
+                        shard_dir=d, keys=second, run="m2")
+    assert len(calls) == 3                       # another run fingerprint reuses nothing
+    with pytest.raises(ValueError):
+        cdist.sweep_sharded(lambda i, ls: fn(i, ls, "q"), 1, [1.0], 2, 2, torch.device("cpu"), shard_dir=d)
 
 
 def _free_port():
@@ -86,6 +121,10 @@ def _inputs(path):
         ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
         out.append((enc["input_ids"][0], wt[0], ans))
     return out
+
+
+def _keys(inputs):
+    return [cdist.unit_key(ids.tolist(), w.float().tolist(), a.tolist()) for ids, w, a in inputs]
 
 
 def _worker(rank, world, port, root, out_path, shard_dir, die_after):
@@ -112,7 +151,7 @@ def _worker(rank, world, port, root, out_path, shard_dir, die_after):
 
     with cpu_ops.patched_ops():
         full = cdist.sweep_sharded(fn, len(inputs), [x[0].numel() for x in inputs], eng.spec.num_layers,
-                                   eng.spec.num_heads, torch.device("cpu"), shard_dir=shard_dir)
+                                   eng.spec.num_heads, torch.device("cpu"), shard_dir=shard_dir, keys=_keys(inputs))
     with open(f"{out_path}.calls{rank}.json", "w") as f:
         json.dump(calls, f)
     if rank == 0:
@@ -161,7 +200,8 @@ def test_resume_after_kill(tmp_path, single):
     out = str(tmp_path / "ie.npy")
     with pytest.raises(Exception):
         _spawn(root, 4, out, shard_dir=shards, die_after=(1, 1))
-    done = cdist.read_shards(shards, one.shape[2])
+    keys = _keys(_inputs(os.path.join(root, __import__("tests.tiny_models").tiny_models.DIR_NAME[KIND])))
+    done = {(keys.index(k), l): row for (k, l), row in cdist.read_shards(shards, one.shape[2]).items()}
     assert 0 < len(done) < NQ * one.shape[1]
     for (q, l), row in done.items():                       # what reached the disk is final
         np.testing.assert_array_equal(np.asarray(row, dtype=np.float32), one[q, l])

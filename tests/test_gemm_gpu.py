@@ -94,3 +94,56 @@ def test_interleave_gate_up_layout():
     wil = ops.interleave_gate_up(wgu, F)[:, 0].long().tolist()
     assert wil[:32] == list(range(32)) and wil[32:64] == list(range(F, F + 32))
     assert wil[64:96] == list(range(32, 64)) and wil[96:] == list(range(F + 32, 2 * F))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K,splits", [
+    (1, 256, 512, 2), (16, 512, 1024, 8), (200, 768, 2048, 4), (256, 1536, 4096, 8), (256, 1024, 4096, 16),
+    (300, 512, 14336, 14), (256, 256, 256, 1), (33, 256, 3584, 7),
+])
+def test_gemm_splitk_store_matches_fp32(gpu_device, dtype, M, N, K, splits):
+    """Split-K form (the decode step's skinny projections): same final-rounding bar as the one-pass GEMM; a second
+    launch is bit-identical (the ranges are added in range order, no atomics)."""
+    x, w = _operands(M, N, K, dtype, gpu_device, 11 * M + N + K + splits)
+    ws = torch.empty(ops.gemm_splitk_workspace_bytes(M, N, splits), dtype=torch.uint8, device=gpu_device)
+    out = ops.gemm_splitk(x, w, splits, workspace=ws)
+    again = ops.gemm_splitk(x, w, splits, workspace=ws)
+    ref = x.float() @ w.float().t()
+    acc_tol = 2.0 ** -22 * (x.float().abs() @ w.float().abs().t())
+    torch.cuda.synchronize()
+    assert torch.equal(out, again)
+    d = (out.float() - ref).abs()
+    assert (d <= _ulp(ref, dtype) + acc_tol).all(), f"max err {d.max().item():.3e}"
+    assert (out == ref.to(dtype)).float().mean().item() >= 0.99
+
+
+def test_gemm_splitk_bias_and_strided_rows(gpu_device):
+    """nn.Linear with bias (Qwen2's q/k/v): out = rnd(x w^T + b); strided activation rows and output rows."""
+    M, N, K = 77, 512, 1024
+    x0, w = _operands(M, N, K + 64, torch.bfloat16, gpu_device, 21)
+    x, w = x0[:, 64:], w[:, :K].contiguous()
+    b = (torch.rand(N, generator=torch.Generator().manual_seed(3)) - 0.5).to(torch.bfloat16).to(gpu_device)
+    big = torch.full((M, N + 64), 7.0, dtype=torch.bfloat16, device=gpu_device)
+    out = big[:, 32:32 + N]
+    ops.gemm_splitk(x, w, 4, bias=b, out=out)
+    ref = x.float() @ w.float().t() + b.float()
+    torch.cuda.synchronize()
+    assert ((out.float() - ref).abs() <= _ulp(ref, torch.bfloat16) + 1e-5).all()
+    assert (big[:, :32] == 7).all() and (big[:, 32 + N:] == 7).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,F,K,splits", [(1, 128, 512, 2), (256, 1024, 4096, 2), (16, 384, 3584, 7)])
+def test_gemm_splitk_silu_mul_cat(gpu_device, dtype, M, F, K, splits):
+    """The MLP activation on the checkpoint's own [gate; up] weight: rnd(rnd(silu(rnd(g))) * rnd(u)), the arithmetic
+    of cram_silu_mul on the rounded projections; bit-identical to split-K STORE followed by cram_silu_mul."""
+    x, wgu = _operands(M, 2 * F, K, dtype, gpu_device, 5 * M + F + K)
+    out = ops.gemm_splitk(x, wgu, splits, ops.GEMM_SILU_MUL_CAT)
+    unfused = ops.silu_mul(ops.gemm_splitk(x, wgu, splits), F)
+    ref = x.float() @ wgu.float().t()
+    exp = _silu_mul_expected(ref[:, :F], ref[:, F:], dtype)
+    torch.cuda.synchronize()
+    assert out.shape == (M, F)
+    assert torch.equal(out, unfused)
+    d = (out.float() - exp.float()).abs()
+    assert (d <= _ulp(exp.float(), dtype) + 1e-6).float().mean().item() >= 0.995
