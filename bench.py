@@ -377,10 +377,15 @@ def main():
                 if os.path.exists(PMC_FILE):
                     pmc = json.load(open(PMC_FILE))
                     ratio = pmc["traffic_over_algorithmic"]
-                    roof["traffic"] = round(ratio * roof["algorithmic_bytes_per_launch"])
-                    roof["traffic_note"] = (f"HBM bytes/launch = PMC (FETCH_SIZEx2 + WRITE_SIZE, {pmc['source']}) "
-                                            f"/ algorithmic = {ratio:.4f} at the sweep shape B=33 T=962, x this run's "
-                                            f"algorithmic bytes per launch")
+                    cur = _b.kernel_source_hash()
+                    if pmc.get("kernel_source_hash") == cur:
+                        roof["traffic"] = round(ratio * roof["algorithmic_bytes_per_launch"])
+                        roof["traffic_note"] = (f"HBM bytes/launch = PMC (FETCH_SIZEx2 + WRITE_SIZE, {pmc['source']}, "
+                                                f"kernel source {cur}) / algorithmic = {ratio:.4f} at the sweep shape "
+                                                f"B=33 T=962, x this run's algorithmic bytes per launch")
+                    else:
+                        roof["traffic_note"] = (f"PMC evidence {pmc['source']} was measured on kernel source "
+                                                f"{pmc.get('kernel_source_hash')}, this build is {cur}: not applied")
             kg = ie["kg"]
             dom = None
             if kg is not None and kg["total_ms"] > 0:

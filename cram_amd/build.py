@@ -71,6 +71,16 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return LIB_PATH
 
 
+def kernel_source_hash() -> str:
+    """Identity of the attention kernels' source (cram_attn.hip, prefill_x64.inc, the ABI header): PMC evidence
+    (profiles/attn_pmc.json) records the hash it was measured on, and bench.py uses it only while it matches."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in (CSRC / "cram_attn.hip", CSRC / "prefill_x64.inc", REPO_DIR / "include" / "cram_attn.h"):
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def x64_asm_path() -> Path:
     """Device assembly of cram_attn.hip saved by the last build (-save-temps=obj)."""
     return PKG_DIR / "build" / f"cram_attn-hip-amdgcn-amd-amdhsa-{ARCH}.s"

@@ -391,6 +391,35 @@ class CrAMEngine:
         return out
 
 
+# Decode-step projections on the split-K matrix-core GEMM (cram_gemm_splitk): rows = the batch (one token per
+# sequence), so a 256-row output tile spans every row and K is cut into ranges until the grid fills the chip.
+# Measured against hipBLASLt with the decode pins (tools/decode_gemm_probe.py, B = 256, weights streamed cold,
+# profiles/r03/decode_gemm_probe_*.jsonl): only the long-K down projection wins (Llama-3 N 4096 x K 14336: 55.9 vs
+# 62.9 us at 8 ranges = 128 workgroups); at K <= N (q/k/v, o_proj, gate/up, lm_head) the fp32 partial slabs and
+# their combine cost more than the library loses, so those stay on F.linear.  CRAM_DECODE_GEMM=0 turns it off (A/B).
+DECODE_GEMM_MAX_ROWS = 512
+DECODE_GEMM_TARGET_WGS = 128
+DECODE_GEMM_MIN_K_OVER_N = 2
+
+
+def decode_splits(N: int, K: int, rows: int) -> int:
+    """K ranges for one decode projection ([rows, K] x [N, K]^T), or 0 for F.linear: for long-K shapes
+    (K >= DECODE_GEMM_MIN_K_OVER_N * N) the count that brings the grid (N / 256 tiles x ranges) nearest
+    DECODE_GEMM_TARGET_WGS workgroups with ranges of >= 256 columns of K."""
+    if os.environ.get("CRAM_DECODE_GEMM", "1") == "0" or rows > DECODE_GEMM_MAX_ROWS or N % 256 or K % 64:
+        return 0
+    if K < DECODE_GEMM_MIN_K_OVER_N * N and os.environ.get("CRAM_DECODE_GEMM") != "all":
+        return 0
+    tiles = N // 256 * -(-rows // 256)
+    best = 0
+    for s in range(1, K // 256 + 1):
+        if K % (64 * s):
+            continue
+        if not best or abs(tiles * s - DECODE_GEMM_TARGET_WGS) < abs(tiles * best - DECODE_GEMM_TARGET_WGS):
+            best = s
+    return best
+
+
 class DecodeSession:
     """Static-shape state of one batched greedy decode (KV cache, bias, token buffers)."""
 
@@ -433,6 +462,29 @@ class DecodeSession:
         self.graph = None
         self.rows = torch.arange(self.B, device=dev)
         self.cos, self.sin = eng.rope_tables(self.S_max)
+        # split-K plan of the step's projections (0 = F.linear) and one workspace shared by all of them (the
+        # step's GEMMs run in stream order)
+        D, F, qkv = sp.hidden, sp.intermediate, sp.q_size + 2 * sp.kv_size
+        self.splits_gemm = {"qkv": decode_splits(qkv, D, self.B), "o": decode_splits(D, sp.q_size, self.B),
+                            "gu": decode_splits(2 * F, D, self.B), "down": decode_splits(D, F, self.B)}
+        shapes = {"qkv": qkv, "o": D, "gu": 2 * F, "down": D}
+        need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in self.splits_gemm.items() if v]
+                   or [0])
+        self.gemm_ws = torch.empty(need, dtype=torch.uint8, device=dev) if need else None
+
+    def _proj(self, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], key: str) -> torch.Tensor:
+        s = self.splits_gemm[key]
+        if s:
+            return ops.gemm_splitk(x, w, s, ops.GEMM_STORE, bias=b, workspace=self.gemm_ws)
+        return ops.linear(x, w, b)
+
+    def _mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
+        s = self.splits_gemm["gu"]
+        if s:
+            act = ops.gemm_splitk(x, lw.wgu, s, ops.GEMM_SILU_MUL_CAT, workspace=self.gemm_ws)
+        else:
+            act = ops.silu_mul(ops.linear(x, lw.wgu), self.eng.spec.intermediate)
+        return self._proj(act, lw.wd, None, "down")
 
     def _pick(self, logits: torch.Tensor, rows: Optional[slice] = None) -> torch.Tensor:
         """Greedy choice as transformers' generate makes it: fp32 logits, the repetition penalty (score / p where
@@ -519,7 +571,7 @@ class DecodeSession:
         self.seq_lens.add_(1)
         for l, lw in enumerate(eng.layers):
             x = eng.rmsnorm(h, lw.ln1)
-            y = ops.linear(x, lw.wqkv, lw.bqkv)                # [B, 1, (Hq + 2 Hkv) d]
+            y = self._proj(x, lw.wqkv, lw.bqkv, "qkv")         # [B, 1, (Hq + 2 Hkv) d]
             # q roped in place; the new token's roped k and its v straight into cache row pos of every sequence
             ops.rope_split(y, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
                            self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2), 0, pos=self.pos,
@@ -528,8 +580,8 @@ class DecodeSession:
             a = ops.attn_decode(q[:, 0], self.k_cache[l], self.v_cache[l], scale=eng.scale, seq_lens=self.seq_lens,
                                 bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
                                 workspace=self.ws)
-            h, x2 = eng.add_rmsnorm(ops.linear(a.flatten(-2)[:, None], lw.wo), h, lw.ln2)
-            h = h + eng.mlp(x2, lw)
+            h, x2 = eng.add_rmsnorm(self._proj(a.flatten(-2)[:, None], lw.wo, None, "o"), h, lw.ln2)
+            h = h + self._mlp(x2, lw)
         hn = eng.rmsnorm(h[:, 0], eng.norm)
         nxt = self._pick(ops.linear(hn, eng.lm_head))
         self.tokens.copy_(nxt)

@@ -123,12 +123,31 @@ def silu_mul(gu, F, out=None):
     return torch.nn.functional.silu(gu[..., :F]) * gu[..., F:]
 
 
+def gemm_splitk_workspace_bytes(M, N, splits):
+    return int(splits) * int(M) * int(N) * 4
+
+
+def gemm_splitk(x, w, splits, epilogue=0, bias=None, workspace=None, out=None, name=None):
+    """cram_gemm_splitk on the CPU: fp32 product (+ bias) rounded once; epilogue 2 = SiLU-mul on [gate; up]."""
+    acc = x.float() @ w.float().t()
+    if epilogue == 2:
+        F = w.shape[0] // 2
+        g = acc[..., :F].to(x.dtype).float()
+        r = (torch.nn.functional.silu(g).to(x.dtype).float() * acc[..., F:].to(x.dtype).float()).to(x.dtype)
+    else:
+        r = (acc + bias.float() if bias is not None else acc).to(x.dtype)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r
+
+
 @contextlib.contextmanager
 def patched_ops():
     """Route cram_amd.ops through the CPU stand-ins for the duration of a CPU test."""
     from cram_amd import ops
     names = ("attn_prefill", "attn_prefill_varlen", "attn_decode", "answer_logits", "decode_workspace_bytes",
-             "rmsnorm", "rope_inplace", "rope_split", "silu_mul")
+             "rmsnorm", "rope_inplace", "rope_split", "silu_mul", "gemm_splitk", "gemm_splitk_workspace_bytes")
     saved = {n: getattr(ops, n) for n in names}
     g = globals()
     for n in names:

@@ -1,0 +1,124 @@
+"""Config 4 end to end at Qwen2-7B's head layout: D 3584, 28 query / 4 kv heads of 128 (GQA-7),
+FFN 18944, q/k/v bias, rope theta 1e6 — two layers of random weights (tests/tiny_models.py kind "qwen2_7b"; the 7-layer
+depth is irrelevant to the kernels, the widths are not) — on one rebuilt TriviaQA prompt (~900 tokens, ideal scores
+[0.1, 1, 1, 1, 1] re-ordered as RAG_test.py:64-107 orders them, all heads re-weighted: layers_to_be_modified = {}).
+
+Pins the automatic GQA-7 choices together at the config's shape: the 7-wave prefill workgroups (hp7, <= 2048 tokens),
+the matrix-core decode for 7-head groups, the q/k/v bias in both the library GEMMs and the decode step's split-K
+GEMM (bias added in its combine), against
+  * the transformers drop-in on the same kernels (greedy ids up to the first near-tie, re_weighting.py:127-132);
+  * the reference hook itself (oracle/hook_ref.py, dense mask, bf16 transformers) and the float32 truth (same hook
+    on the float32 copy of the weights): re-weighted answer log-probs of the drop-in and of the engine within
+    2.5 x the reference's own bf16 error + 0.01 (the G6 bar of test_dropin_gpu.py).
+"""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests import tiny_models as tm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def qwen7(tmp_path_factory, gpu_device):
+    from cram_amd import scores as SC
+    from cram_amd.re_weighting import Re_Weighting_Strategy
+    root = str(tmp_path_factory.mktemp("qwen7"))
+    path, path32 = tm.save_model("qwen2_7b", root), tm.save_model("qwen2_7b", root, fp32=True)
+    with gzip.open(os.path.join(tm.REPO, "data", "trivia_1000.json.gz"), "rt", encoding="utf-8") as f:
+        data = json.load(f)
+    obj = Re_Weighting_Strategy(model_name=path, layers_to_be_modified={})
+    # the two prompts nearest 920 tokens among the first 64 (config 4's mean is ~919)
+    cands = []
+    for i in range(64):
+        paras, sc = SC.assemble(data[i], ideal=True, ideal_score=1)
+        enc, _ = obj.decode_with_special_attention(question=data[i]["question"], paras=paras, scores=sc)
+        cands.append((abs(enc["input_ids"].shape[1] - 920), i, paras, sc))
+    cands.sort(key=lambda x: x[:2])
+    recs = [(data[i], paras, sc) for _, i, paras, sc in cands[:2]]
+    yield obj, path32, recs
+    del obj
+    torch.cuda.empty_cache()
+
+
+def _gaps(scores):
+    return [float(torch.topk(s[0].float(), 2).values.diff().abs()) for s in scores]
+
+
+def test_config4_shape_selects_the_gqa7_kernels(qwen7):
+    obj, _, recs = qwen7
+    sp = obj.engine.spec
+    assert (sp.hidden, sp.num_heads, sp.num_kv_heads, sp.head_dim, sp.intermediate, sp.qkv_bias) == \
+        (3584, 28, 4, 128, 18944, True)
+    enc, _ = obj.decode_with_special_attention(question=recs[0][0]["question"], paras=recs[0][1], scores=recs[0][2])
+    assert 700 < enc["input_ids"].shape[1] < 1200
+
+
+def test_config4_engine_decode_matches_dropin(qwen7):
+    """run_RAG_batch (engine: packed varlen prefill, graph-replayed steps, split-K decode projections with the q/k/v
+    bias) == the transformers drop-in's model.generate on the cram_hip kernels, up to the first near-tie."""
+    from cram_amd import attention as A
+    obj, _, recs = qwen7
+    heads = obj.layers_to_be_modified
+    qs, ps, ss = [r[0]["question"] for r in recs], [r[1] for r in recs], [r[2] for r in recs]
+    batched = obj.run_RAG_batch(qs, ps, ss, max_new_tokens=16, use_graph=True)
+    assert batched == obj.run_RAG_batch(qs, ps, ss, max_new_tokens=16, use_graph=False)
+    eos = obj._generate_kwargs().get("eos_token_id", obj.model.generation_config.eos_token_id)
+    eos = [eos] if isinstance(eos, int) else list(eos or [])
+    compared = 0
+    for q, p, s in zip(qs, ps, ss):
+        enc, w = obj.decode_with_special_attention(question=q, paras=p, scores=s)
+        cb = obj._bias(w, heads)
+        with A.reweighting(obj.model, cb), torch.no_grad():
+            out = obj.model.generate(**enc, do_sample=False, max_new_tokens=16, output_scores=True,
+                                     return_dict_in_generate=True, eos_token_id=eos)
+        ref = out.sequences[0, enc["input_ids"].shape[1]:].tolist()
+        got = obj.engine.generate([enc["input_ids"][0]], [w.cpu()], heads, max_new_tokens=16, eos_ids=eos)[0]
+        gaps = _gaps(out.scores)
+        for t in range(min(len(ref), len(got))):
+            if ref[t] != got[t]:
+                assert min(gaps[:t + 1]) < 0.05, (t, gaps[t])
+                break
+            compared += 1
+    print(f"\nconfig-4 shape: {compared} greedy tokens equal before any near-tie")
+    assert compared >= 4
+
+
+def test_config4_answer_logprobs_match_reference_hook(qwen7):
+    """Drop-in (transformers + cram_hip) and engine (fused forward) re-weighted answer log-probs vs the reference
+    hook in bf16 and the float32 truth, on the same GPU."""
+    from transformers import AutoModelForCausalLM
+    from oracle import hook_ref
+    obj, path32, recs = qwen7
+    dev = obj.device
+    m16 = AutoModelForCausalLM.from_pretrained(obj.model_name, dtype="auto", attn_implementation="sdpa").to(dev).eval()
+    m32 = AutoModelForCausalLM.from_pretrained(path32, dtype="auto", attn_implementation="sdpa").to(dev).eval()
+    L, H = obj.num_hidden_layers, obj.model_num_attention_heads
+    heads = {l: list(range(H)) for l in range(L)}
+    eng = obj.engine
+    try:
+        for rec, paras, sc in recs:
+            ans = rec["wrong_answer"]
+            lp = obj.answer_logprobs(question=rec["question"], paras=paras, scores=sc, answer=ans).cpu().numpy()
+            enc, w = obj.decode_with_special_attention(question=rec["question"], paras=paras, scores=sc, answer=ans)
+            ids = enc["input_ids"]
+            n, T = lp.size, ids.shape[1]
+            lw = hook_ref.log_weight(w)
+            truth = hook_ref.answer_logprobs(m32, ids, lw, heads, n).cpu().numpy()
+            ref = hook_ref.answer_logprobs(m16, ids, lw, heads, n).cpu().numpy()
+            cb = obj._bias(w, obj.layers_to_be_modified)
+            lg = eng.logits(ids, cb, last=n + 1)[0, :n].float()
+            el = torch.log_softmax(lg, -1).gather(1, ids[0, T - n:].view(n, 1)).view(n).cpu().numpy()
+            ref_err = np.abs(ref - truth).max()
+            print(f"\nT={T} n={n}: |drop-in - truth| {np.abs(lp - truth).max():.4f}, |engine - truth| "
+                  f"{np.abs(el - truth).max():.4f}, reference bf16 error {ref_err:.4f}")
+            assert np.abs(lp - truth).max() <= 2.5 * ref_err + 0.01
+            assert np.abs(el - truth).max() <= 2.5 * ref_err + 0.01
+    finally:
+        del m16, m32
+        torch.cuda.empty_cache()

@@ -206,6 +206,25 @@ def test_engine_batched_generate_matches_single(tiny, nq):
         chunked.prefill(max_rows=340)
         whole.prefill()
     assert both == one
+    # the decode step's projections on the split-K GEMM (cram_gemm_splitk; CRAM_DECODE_GEMM=all routes every
+    # projection of the tiny shapes through it) == F.linear
+    os.environ["CRAM_DECODE_GEMM"] = "all"
+    try:
+        with cpu_ops.patched_ops():
+            sk = DecodeSession(eng, prompts, ws, heads, 5)
+            assert all(sk.splits_gemm.values()), sk.splits_gemm
+            allk = eng.generate(prompts, ws, heads, max_new_tokens=5, use_graph=False)
+    finally:
+        os.environ.pop("CRAM_DECODE_GEMM")
+    assert allk == both
+    os.environ["CRAM_DECODE_GEMM"] = "0"
+    try:
+        with cpu_ops.patched_ops():
+            lib = eng.generate(prompts, ws, heads, max_new_tokens=5, use_graph=False)
+            assert not any(DecodeSession(eng, prompts, ws, heads, 5).splits_gemm.values())
+    finally:
+        os.environ.pop("CRAM_DECODE_GEMM")
+    assert lib == both
     assert chunked.tokens.tolist() == whole.tokens.tolist() == [r[0] for r in both]
     assert torch.equal(chunked.k_cache, whole.k_cache) and torch.equal(chunked.v_cache, whole.v_cache)
     # and against the hooked transformers model

@@ -146,4 +146,7 @@ def test_gemm_splitk_silu_mul_cat(gpu_device, dtype, M, F, K, splits):
     assert out.shape == (M, F)
     assert torch.equal(out, unfused)
     d = (out.float() - exp.float()).abs()
-    assert (d <= _ulp(exp.float(), dtype) + 1e-6).float().mean().item() >= 0.995
+    # a 1-ulp difference of each rounded projection propagates through silu and the product: every element within
+    # 4 ulp, >= 99 % within 1 (M = 1 has only 128 elements)
+    assert (d <= 4 * _ulp(exp.float(), dtype) + 1e-6).all(), float((d / _ulp(exp.float(), dtype)).max())
+    assert (d <= _ulp(exp.float(), dtype) + 1e-6).float().mean().item() >= 0.99

@@ -21,7 +21,9 @@ TOK_DIR = {"llama3": os.path.join(REPO, "data", "tok_llama3"), "qwen2": os.path.
            "gpt2": os.path.join(REPO, "data", "tok_llama3"), "llama2": os.path.join(REPO, "data", "tok_llama3")}
 # names select the reference's chat branch; "gpt2-tiny" and "Llama-2-tiny" match neither, i.e. the
 # raw-template branch (the reference's default model, Llama-2-13b-chat-hf, takes that branch too)
-DIR_NAME = {"llama3": "Llama-3-tiny", "qwen2": "Qwen2-tiny", "gpt2": "gpt2-tiny", "llama2": "Llama-2-tiny"}
+DIR_NAME = {"llama3": "Llama-3-tiny", "qwen2": "Qwen2-tiny", "gpt2": "gpt2-tiny", "llama2": "Llama-2-tiny",
+            "qwen2_7b": "Qwen2-7B-heads-2layer"}
+TOK_DIR["qwen2_7b"] = TOK_DIR["qwen2"]
 DTYPE = {"llama2": torch.float16}
 
 SPECS = {
@@ -37,7 +39,14 @@ SPECS = {
     "llama2": dict(hidden_size=256, intermediate_size=512, num_hidden_layers=3, num_attention_heads=4,
                    num_key_value_heads=4, head_dim=128, rope_theta=10000.0, rms_norm_eps=1e-5,
                    max_position_embeddings=4096, tie_word_embeddings=False),
+    # config 4's layout at full width (Qwen2-7B: D 3584, 28 q / 4 kv heads of 128, FFN 18944, q/k/v bias,
+    # rope 1e6), two layers: the GQA-7 kernels and the decode projections at their real shapes
+    "qwen2_7b": dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=2, num_attention_heads=28,
+                     num_key_value_heads=4, rope_theta=1000000.0, rms_norm_eps=1e-6,
+                     max_position_embeddings=4096, tie_word_embeddings=False),
 }
+# linear-weight std per kind (fan-in 256 for the tiny kinds; the full-width kind keeps the activations O(1))
+LIN_STD_KIND = {"qwen2_7b": 0.02}
 SEED = 20250404
 LIN_STD = 0.08
 
@@ -92,7 +101,7 @@ def build_model(kind: str, attn_implementation: str = "sdpa"):
         elif name.endswith(".bias"):
             sd[name] = draw(name, tuple(p.shape), 0.05)
         else:
-            sd[name] = draw(name, tuple(p.shape), LIN_STD)
+            sd[name] = draw(name, tuple(p.shape), LIN_STD_KIND.get(kind, LIN_STD))
     model.load_state_dict(sd)
     model.eval()
     return model

@@ -10,6 +10,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cram_amd.build import kernel_source_hash  # noqa: E402
 from cram_amd.ops import prefill_work  # noqa: E402
 
 src = sys.argv[1] if len(sys.argv) > 1 else "profiles/r01_pmc"
@@ -30,6 +31,7 @@ out = {"kernel": "prefill_kernel<128>", "shape": {"B": B, "T": T, "Hq": Hq, "Hkv
        "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "hbm_read_bytes": read_b, "hbm_write_bytes": write_b,
        "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
        "traffic_over_algorithmic": (read_b + write_b) / alg, "source": src,
+       "kernel_source_hash": kernel_source_hash(),
        "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc_attn.sh); FETCH_SIZE x2 "
                "(gfx950 16B/lane read undercount), KiB -> B"}
 json.dump(out, open("profiles/attn_pmc.json", "w"), indent=1)
