@@ -569,8 +569,12 @@ class DecodeSession:
         eng, sp = self.eng, self.eng.spec
         h = eng.embed[self.tokens][:, None]                      # [B, 1, D]
         self.seq_lens.add_(1)
+        m = None                    # pending MLP output: the residual add runs inside the next RMSNorm
         for l, lw in enumerate(eng.layers):
-            x = eng.rmsnorm(h, lw.ln1)
+            if m is None:
+                x = eng.rmsnorm(h, lw.ln1)
+            else:
+                h, x = eng.add_rmsnorm(m, h, lw.ln1)
             y = self._proj(x, lw.wqkv, lw.bqkv, "qkv")         # [B, 1, (Hq + 2 Hkv) d]
             # q roped in place; the new token's roped k and its v straight into cache row pos of every sequence
             ops.rope_split(y, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
@@ -581,8 +585,8 @@ class DecodeSession:
                                 bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
                                 workspace=self.ws)
             h, x2 = eng.add_rmsnorm(self._proj(a.flatten(-2)[:, None], lw.wo, None, "o"), h, lw.ln2)
-            h = h + self._mlp(x2, lw)
-        hn = eng.rmsnorm(h[:, 0], eng.norm)
+            m = self._mlp(x2, lw)
+        _, hn = eng.add_rmsnorm(m[:, 0], h[:, 0], eng.norm)
         nxt = self._pick(ops.linear(hn, eng.lm_head))
         self.tokens.copy_(nxt)
         self.out.index_copy_(1, self.t.view(1), nxt[:, None])
