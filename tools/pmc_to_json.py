@@ -18,7 +18,10 @@ B, T, Hq, Hkv, d = 33, 962, 32, 8, 128
 
 
 def mean(name, f):
-    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(src, f))) if r["Counter_Name"] == name]
+    import glob
+    hits = [os.path.join(src, f)] if os.path.exists(os.path.join(src, f)) else \
+        sorted(glob.glob(os.path.join(src, "**", f), recursive=True))
+    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(hits[0])) if r["Counter_Name"] == name]
     return sum(v) / len(v), len(v)
 
 
