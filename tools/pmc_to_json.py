@@ -33,7 +33,8 @@ _, alg = prefill_work(B, Hq, Hkv, T, T, d, 0)
 out = {"kernel": "prefill_kernel<128>", "shape": {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d}, "dispatches": n,
        "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "hbm_read_bytes": read_b, "hbm_write_bytes": write_b,
        "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
-       "traffic_over_algorithmic": (read_b + write_b) / alg, "source": src,
+       "traffic_over_algorithmic": (read_b + write_b) / alg,
+       "source": os.path.relpath(os.path.abspath(src), os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
        "kernel_source_hash": kernel_source_hash(),
        "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc_attn.sh); FETCH_SIZE x2 "
                "(gfx950 16B/lane read undercount), KiB -> B"}
