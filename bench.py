@@ -366,9 +366,11 @@ def main():
             roof = None
             if kt is not None and kt["total_ms"] > 0:
                 ach = kt["flops"] / (kt["total_ms"] * 1e-3) / 1e12
+                kname = ops.prefill_kernel_name(result["dtype"], spec.num_heads, spec.num_kv_heads,
+                                                int(ie["work"][0][1].numel()))
                 roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                        "kernel": f"prefill_kernel<{result['dtype']}, 128> (credibility-biased causal GQA flash "
+                        "kernel": f"{kname} ({result['dtype']}, d = 128: credibility-biased causal GQA flash "
                                   f"attention, {result['dtype']} MFMA)",
                         "launches": kt["launches"], "avg_launch_ms": round(kt["avg_ms"], 4),
                         "flops_per_launch": kt["flops"] / kt["launches"],

@@ -18,7 +18,7 @@ REPO_DIR = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc"
 LIB_PATH = PKG_DIR / "libcram_attn.so"
 SOURCES = [CSRC / "cram_attn.hip", CSRC / "cram_fused.hip", CSRC / "cram_gemm.hip", CSRC / "cram_spans.cpp"]
-HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_x64.inc"]
+HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc"]
 ARCH = "gfx950"
 
 
@@ -59,10 +59,11 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     failed = [cmd for p, cmd in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    bad = audit_x64(x64_asm_path().read_text())
-    if bad:
-        raise RuntimeError("prefill_x64_kernel register audit failed (the library is not installed): "
-                           + "; ".join(bad[:5]))
+    asm = x64_asm_path().read_text()
+    for kname in ASM_KERNELS:
+        bad = audit_x64(asm, kname)
+        if bad:
+            raise RuntimeError(f"{kname} register audit failed (the library is not installed): " + "; ".join(bad[:5]))
     link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(tmp)]
     if verbose:
         print(" ".join(link), file=sys.stderr)
@@ -76,7 +77,7 @@ def kernel_source_hash() -> str:
     (profiles/attn_pmc.json) records the hash it was measured on, and bench.py uses it only while it matches."""
     import hashlib
     h = hashlib.sha256()
-    for f in (CSRC / "cram_attn.hip", CSRC / "prefill_x64.inc", REPO_DIR / "include" / "cram_attn.h"):
+    for f in (CSRC / "cram_attn.hip", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc", REPO_DIR / "include" / "cram_attn.h"):
         h.update(f.read_bytes())
     return h.hexdigest()[:16]
 
@@ -104,14 +105,19 @@ def _sgprs(op: str) -> set:
 _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "s_barrier", "s_setprio", "s_endpgm")
 
 
-def audit_x64(asm: str) -> list:
+# kernels that own accumulator registers by name inside their inline asm (x64: O = a[0:127], Q = a[128:191];
+# x32: O = a[0:63], Q = a[64:95])
+ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernel")
+
+
+def audit_x64(asm: str, kname: str = "prefill_x64_kernel") -> list:
     """prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]) inside its inline asm;
     hipcc knows nothing of that.  Returns the violations (empty = clean):
       * any v_accvgpr_* / AGPR operand the COMPILER emitted (outside the kernel's ;;#ASMSTART..;;#ASMEND blocks);
       * any scratch traffic in the kernel;
       * an LDS-DMA whose descriptor SGPRs were written by a VALU op fewer than 5 wait states earlier (the kernel's
         DMA pieces after the first of a tile carry no s_nop of their own)."""
-    body = kernel_body(asm, "prefill_x64_kernel")
+    body = kernel_body(asm, kname)
     bad = []
     inside = False
     for line in body.splitlines():
@@ -123,7 +129,7 @@ def audit_x64(asm: str) -> list:
         elif t and not t.startswith((";", ".")) and not inside and ("accvgpr" in t or re.search(r"\ba\[?\d", t)):
             bad.append("compiler AGPR use: " + t)
     if "scratch_" in body:
-        bad.append("scratch traffic in prefill_x64_kernel")
+        bad.append(f"scratch traffic in {kname}")
     ins = [t.strip() for t in body.splitlines()]
     ins = [t.replace(",", " ").split() for t in ins if t and not t.startswith((";", "."))]
     n_dma = 0

@@ -50,6 +50,21 @@ class KernelTimer:
 TIMER = KernelTimer()
 
 
+def prefill_kernel_name(dtype: str, Hq: int, Hkv: int, Tq: int, d: int = 128) -> str:
+    """The kernel cram_prefill launches for such a call under the current knob (the selection rule of launch_prefill,
+    csrc/cram_attn.hip; labels the bench line's roofline kernel)."""
+    kv = _lib.get_knob(_lib.KNOB_PREFILL_VARIANT)
+    G = Hq // Hkv
+    if d == 128 and dtype == "bf16" and G % 4 == 0:
+        if kv == 6:
+            return "prefill_x64_kernel"
+        if kv == 4 or (kv == -1 and Tq >= 256):
+            return "prefill_x32_kernel"
+    if d == 128 and G % 7 == 0 and (kv == 7 or (kv == -1 and Tq <= 2048)):
+        return "prefill_kernel<7 waves>"
+    return {3: "prefill_kernel<32-key tiles>", 8: "prefill_kernel<8 waves>"}.get(kv, "prefill_kernel")
+
+
 def prefill_work(B, Hq, Hkv, Tq, S, d, q_pos0):
     """Algorithmic flops and HBM bytes of one causal prefill launch."""
     visible = Tq * q_pos0 + Tq * (Tq + 1) / 2.0            # sum over queries of visible keys

@@ -65,10 +65,11 @@ int cram_abi_version(void);
  * the first query (once per process, thread-safe); no launch reads the environment.  Knob values are atomics:
  * a value set from one thread is seen by launches issued afterwards from any thread.
  *   CRAM_KNOB_PREFILL_VARIANT  -1 = automatic: 64-key tiles, 4 waves, except GQA-7 groups with sequences <= 2048
- *                              (7-wave workgroups) and bf16 GQA groups of 4k with >= 4096 query rows (variant 6);
+ *                              (7-wave workgroups) and bf16 d = 128 GQA groups of 4k with >= 256 query rows (variant 4);
  *                              0 = always 4 waves; 3 = 32-key tiles; 8 = 8-wave workgroups;
  *                              7 = 7-wave workgroups for GQA-7 groups; 6 = one wave per SIMD, 64 rows per wave
- *                              (bf16, d = 128, GQA groups of 4k; otherwise as 0)
+ *                              (bf16, d = 128, GQA groups of 4k; otherwise as 0); 4 = two workgroups per CU, 32 rows
+ *                              per wave, hand-ordered stream (bf16, d = 128, GQA groups of 4k; otherwise as 0)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
  * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob stores the value in

@@ -1,5 +1,6 @@
-"""prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]); hipcc knows nothing of that
-ownership, so a compiler spill or copy into the AGPR file would silently corrupt O or Q.  cram_amd.build runs the audit
+"""prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]), and so does
+prefill_x32_kernel (O = a[0:63], Q = a[64:95]); hipcc knows nothing of that ownership, so a compiler spill or copy into
+the AGPR file would silently corrupt O or Q.  cram_amd.build runs the audit
 (cram_amd.build.audit_x64) on the device assembly of every build it makes and refuses to install a library that fails
 it; this CPU test re-checks the assembly of the current build: no v_accvgpr_* instruction or AGPR operand outside the
 kernel's own inline-asm statements, no scratch traffic, and 5 wait states between any VALU write of an LDS-DMA
@@ -23,11 +24,14 @@ def asm():
     return build.x64_asm_path().read_text()
 
 
-def test_x64_kernel_register_ownership_and_dma_hazards(asm):
-    assert build.audit_x64(asm) == []
+@pytest.mark.parametrize("kname", build.ASM_KERNELS)
+def test_asm_kernel_register_ownership_and_dma_hazards(asm, kname):
+    assert build.audit_x64(asm, kname) == []
 
 
-def test_audit_catches_a_compiler_agpr_and_scratch_traffic(asm):
-    body = build.kernel_body(asm, "prefill_x64_kernel")
-    assert build.audit_x64(asm.replace(body, body + "\n\tv_accvgpr_write_b32 a5, v1\n", 1))
-    assert any("scratch" in b for b in build.audit_x64(asm.replace(body, body + "\n\tscratch_store_dword v0, v1, off\n", 1)))
+@pytest.mark.parametrize("kname", build.ASM_KERNELS)
+def test_audit_catches_a_compiler_agpr_and_scratch_traffic(asm, kname):
+    body = build.kernel_body(asm, kname)
+    assert build.audit_x64(asm.replace(body, body + "\n\tv_accvgpr_write_b32 a5, v1\n", 1), kname)
+    assert any("scratch" in b for b in build.audit_x64(asm.replace(body, body + "\n\tscratch_store_dword v0, v1, off\n",
+                                                                                 1), kname))

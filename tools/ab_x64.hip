@@ -1,9 +1,10 @@
-// A/B and agreement check of prefill_x64_kernel (one wave per SIMD, 64 rows per wave) against the library's
-// prefill_kernel on the same inputs, in one process:
+// A/B and agreement check of prefill_x64_kernel (one wave per SIMD, 64 rows per wave) and prefill_x32_kernel (two
+// workgroups per CU, 32 rows per wave) against the library's prefill_kernel on the same inputs, in one process:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/ab_x64.hip -o tools/ab_x64 && tools/ab_x64
 // Cases: the IE-sweep shape (B=33, T=962, Llama-3 GQA 32/8, d 128, fused QKV layout), a suffix-style call (queries at
 // positions p0.., keys 0..p0+T), a biased call (some heads enabled, -inf and log 0.1 spans), the 8.3k-token prompt.
-// Prints max |x64 - library| and both kernels' times (median of 5 rounds of 10 launches each, interleaved).
+// Prints max |x - library| and the kernels' times (median of 5 rounds of 10 launches each, interleaved).
+// -DCRAM_X64_STAMPS / -DCRAM_X32_STAMPS: per-phase cycle stamps of that kernel.
 #include "../cram_amd/csrc/cram_attn.hip"
 
 #include <algorithm>
@@ -72,11 +73,11 @@ int main(int argc, char** argv) {
         for (int h = 0; h < c.Hq; ++h) he[(size_t)b * c.Hq + h] = ((h * 7 + b) % 3) != 0;
       }
     }
-    __bf16 *q, *k, *v, *o1, *o2;
+    __bf16 *q, *k, *v, *o1, *o2, *o3;
     float* bias;
     uint8_t* en;
     CK(hipMalloc(&q, nq * 2)); CK(hipMalloc(&k, nkv * 2)); CK(hipMalloc(&v, nkv * 2));
-    CK(hipMalloc(&o1, no * 2)); CK(hipMalloc(&o2, no * 2));
+    CK(hipMalloc(&o1, no * 2)); CK(hipMalloc(&o2, no * 2)); CK(hipMalloc(&o3, no * 2));
     CK(hipMalloc(&bias, hb.size() * 4)); CK(hipMalloc(&en, he.size()));
     CK(hipMemcpy(q, hq.data(), nq * 2, hipMemcpyHostToDevice));
     CK(hipMemcpy(k, hk.data(), nkv * 2, hipMemcpyHostToDevice));
@@ -85,6 +86,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(en, he.data(), he.size(), hipMemcpyHostToDevice));
     CK(hipMemset(o1, 0, no * 2));
     CK(hipMemset(o2, 0, no * 2));
+    CK(hipMemset(o3, 0, no * 2));
 
     PrefillParams p{};
     p.q = q; p.q_sb = (int64_t)c.T * N; p.q_sh = d; p.q_st = N;
@@ -96,36 +98,42 @@ int main(int argc, char** argv) {
     p.B = c.B; p.Hq = c.Hq; p.Hkv = c.Hkv; p.Tq = c.T; p.S = S; p.W = W; p.q_pos0 = c.p0;
     p.scale_log2 = kLog2e / sqrtf((float)d);
     p.cu = nullptr;
-    PrefillParams p1 = p, p2 = p;
+    PrefillParams p1 = p, p2 = p, p3 = p;
     p1.o = o1; p1.hp = 4; p1.nqb = (c.T + 31) / 32; p1.nblocks = p1.nqb * (c.Hq / 4) * c.B;
     p2.o = o2; p2.hp = 4; p2.nqb = (c.T + 63) / 64; p2.nblocks = p2.nqb * (c.Hq / 4) * c.B;
+    p3.o = o3; p3.hp = 4; p3.nqb = (c.T + 31) / 32; p3.nblocks = p3.nqb * (c.Hq / 4) * c.B;
     auto run = [&](int which) {
       if (which == 0)
         hipLaunchKernelGGL((prefill_kernel<__bf16, 128, 64, 2>), dim3(p1.nblocks), dim3(256), 0, 0, p1);
-      else
+      else if (which == 1)
         hipLaunchKernelGGL(prefill_x64_kernel, dim3(p2.nblocks), dim3(256), 0, 0, p2);
+      else
+        hipLaunchKernelGGL(prefill_x32_kernel, dim3(p3.nblocks), dim3(256), 0, 0, p3);
     };
     run(0);
     run(1);
+    run(2);
     CK(hipDeviceSynchronize());
     std::vector<__bf16> a(no), bb(no);
     CK(hipMemcpy(a.data(), o1, no * 2, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(bb.data(), o2, no * 2, hipMemcpyDeviceToHost));
-    double md = 0, sd = 0;
-    size_t nbad = 0, nnan = 0;
-    for (size_t i = 0; i < no; ++i) {
-      const double x = (float)a[i], y = (float)bb[i];
-      if (std::isnan(y) || std::isinf(y)) { ++nnan; continue; }
-      const double e = fabs(x - y);
-      md = std::max(md, e);
-      sd += e;
-      if (e > 2e-2 + 2e-2 * fabs(x)) ++nbad;
+    double md[3] = {}, sd[3] = {};
+    size_t nbad[3] = {}, nnan[3] = {};
+    for (int w = 1; w < 3; ++w) {
+      CK(hipMemcpy(bb.data(), w == 1 ? o2 : o3, no * 2, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < no; ++i) {
+        const double x = (float)a[i], y = (float)bb[i];
+        if (std::isnan(y) || std::isinf(y)) { ++nnan[w]; continue; }
+        const double e = fabs(x - y);
+        md[w] = std::max(md[w], e);
+        sd[w] += e;
+        if (e > 2e-2 + 2e-2 * fabs(x)) ++nbad[w];
+      }
     }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    std::vector<float> t[2];
+    std::vector<float> t[3];
     for (int rnd = 0; rnd < 5; ++rnd)
-      for (int w = 0; w < 2; ++w) {
+      for (int w = 0; w < 3; ++w) {
         CK(hipEventRecord(e0));
         for (int i = 0; i < iters; ++i) run(w);
         CK(hipEventRecord(e1));
@@ -158,14 +166,39 @@ int main(int argc, char** argv) {
       CK(hipFree(st));
     }
 #endif
+#ifdef CRAM_X32_STAMPS
+    {
+      unsigned long long* st;
+      const size_t ns = (size_t)p3.nblocks * 4 * 8;
+      CK(hipMalloc(&st, ns * 8));
+      CK(hipMemset(st, 0, ns * 8));
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_x32_stamps), &st, sizeof(st)));
+      run(2);
+      CK(hipDeviceSynchronize());
+      std::vector<unsigned long long> hs(ns);
+      CK(hipMemcpy(hs.data(), st, ns * 8, hipMemcpyDeviceToHost));
+      double sum[8] = {};
+      for (size_t w = 0; w < (size_t)p3.nblocks * 4; ++w)
+        for (int k = 0; k < 6; ++k) sum[k] += (double)hs[w * 8 + k];
+      const double nw = (double)p3.nblocks * 4, steps = sum[4];
+      printf("  x32 stamps per wave: prologue %.0f, epilogue %.0f cycles; per step: A %.0f, B %.0f (R wait+barrier "
+             "%.0f) (steps/wave %.1f)\n", sum[0] / nw, sum[5] / nw, sum[1] / steps, sum[2] / steps, sum[3] / steps,
+             steps / nw);
+      unsigned long long* nul = nullptr;
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_x32_stamps), &nul, sizeof(nul)));
+      CK(hipFree(st));
+    }
+#endif
     const double fl = flops_of(c);
-    const bool ok = nbad == 0 && nnan == 0;
+    const bool ok = nbad[1] == 0 && nnan[1] == 0 && nbad[2] == 0 && nnan[2] == 0;
     all_ok &= ok;
-    printf("%-26s lib %.3f ms (%5.0f TF/s)  x64 %.3f ms (%5.0f TF/s)  x%.3f   max|diff| %.2e mean %.2e bad %zu nan %zu %s\n",
-           c.name, t[0][2], fl / t[0][2] / 1e9, t[1][2], fl / t[1][2] / 1e9, t[0][2] / t[1][2], md, sd / no, nbad, nnan,
+    printf("%-26s lib %.3f ms (%5.0f TF/s) | x64 %.3f ms (%5.0f) x%.3f max|d| %.2e mean %.2e bad %zu nan %zu | "
+           "x32 %.3f ms (%5.0f) x%.3f max|d| %.2e mean %.2e bad %zu nan %zu %s\n",
+           c.name, t[0][2], fl / t[0][2] / 1e9, t[1][2], fl / t[1][2] / 1e9, t[0][2] / t[1][2], md[1], sd[1] / no,
+           nbad[1], nnan[1], t[2][2], fl / t[2][2] / 1e9, t[0][2] / t[2][2], md[2], sd[2] / no, nbad[2], nnan[2],
            ok ? "OK" : "MISMATCH");
     fflush(stdout);
-    CK(hipFree(q)); CK(hipFree(k)); CK(hipFree(v)); CK(hipFree(o1)); CK(hipFree(o2)); CK(hipFree(bias)); CK(hipFree(en));
+    CK(hipFree(q)); CK(hipFree(k)); CK(hipFree(v)); CK(hipFree(o1)); CK(hipFree(o2)); CK(hipFree(o3)); CK(hipFree(bias)); CK(hipFree(en));
   }
   return all_ok ? 0 : 2;
 }

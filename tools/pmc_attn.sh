@@ -8,7 +8,7 @@ mkdir -p $OUT
 ARGS="${@:-}"
 run() {
   name=$1; shift
-  timeout -k 10 180 rocprofv3 --kernel-include-regex prefill_kernel --pmc "$@" --kernel-trace --output-format csv \
+  timeout -k 10 180 rocprofv3 --kernel-include-regex 'prefill_(x32_|x64_)?kernel' --pmc "$@" --kernel-trace --output-format csv \
     -d $OUT/$name -o $name -- python3 tools/prof_attn.py --iters 5 $ARGS > $OUT/$name.log 2>&1
 }
 run p1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES

@@ -17,11 +17,16 @@ src = sys.argv[1] if len(sys.argv) > 1 else "profiles/r01_pmc"
 B, T, Hq, Hkv, d = 33, 962, 32, 8, 128
 
 
+KERNELS = set()
+
+
 def mean(name, f):
     import glob
     hits = [os.path.join(src, f)] if os.path.exists(os.path.join(src, f)) else \
         sorted(glob.glob(os.path.join(src, "**", f), recursive=True))
-    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(hits[0])) if r["Counter_Name"] == name]
+    rows = [r for r in csv.DictReader(open(hits[0])) if r["Counter_Name"] == name]
+    KERNELS.update(r.get("Kernel_Name", "?") for r in rows)
+    v = [float(r["Counter_Value"]) for r in rows]
     return sum(v) / len(v), len(v)
 
 
@@ -30,7 +35,7 @@ write_kib, _ = mean("WRITE_SIZE", "p4_counter_collection.csv")
 read_b = fetch_kib * 1024 * 2
 write_b = write_kib * 1024
 _, alg = prefill_work(B, Hq, Hkv, T, T, d, 0)
-out = {"kernel": "prefill_kernel<128>", "shape": {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d}, "dispatches": n,
+out = {"kernel": " / ".join(sorted(KERNELS)), "shape": {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d}, "dispatches": n,
        "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "hbm_read_bytes": read_b, "hbm_write_bytes": write_b,
        "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
        "traffic_over_algorithmic": (read_b + write_b) / alg,
