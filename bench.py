@@ -151,7 +151,10 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    ap.add_argument("--decode-batch", type=int, default=256)
+    # NQ-1000 on one GPU = two batches of 500: 512 prompts per GPU share every decode step's 15 GB weight read (the M = 512
+    # projections run near the matrix-core rate, M = 256 ones at 1.5-4 TB/s of weights); the KV cache of 512 rows is
+    # 69 GB of the 288 GB (round 3: 72.4 vs 67.9 questions/s at 256 on one box, profiles/r03/s5_probe1/)
+    ap.add_argument("--decode-batch", type=int, default=512)
     ap.add_argument("--decode-tokens", type=int, default=100, help="new tokens per question (re_weighting.py:127)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--scores", default="ideal", choices=["ideal", "gpt"],
