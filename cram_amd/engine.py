@@ -404,14 +404,15 @@ DECODE_GEMM_MIN_K_OVER_N = 2
 
 def decode_splits(N: int, K: int, rows: int) -> int:
     """K ranges for one decode projection ([rows, K] x [N, K]^T), or 0 for F.linear: for long-K shapes
-    (K >= DECODE_GEMM_MIN_K_OVER_N * N) the count that brings the grid (N / 256 tiles x ranges) nearest
-    DECODE_GEMM_TARGET_WGS workgroups with ranges of >= 256 columns of K."""
+    (K >= DECODE_GEMM_MIN_K_OVER_N * N) the count that brings N / 256 column tiles x ranges nearest
+    DECODE_GEMM_TARGET_WGS with ranges of >= 256 columns of K (the same count at every row count up to
+    DECODE_GEMM_MAX_ROWS)."""
     if os.environ.get("CRAM_DECODE_GEMM", "1") == "0" or rows > DECODE_GEMM_MAX_ROWS or N % 256 or K % 64:
         return 0
     if K < DECODE_GEMM_MIN_K_OVER_N * N and os.environ.get("CRAM_DECODE_GEMM") != "all":
         return 0
-    tiles = N // 256 * -(-rows // 256)
-    best = 0
+    tiles = N // 256          # column tiles; the row tiles (rows > 256) are not counted: 8 ranges won at both 256 and
+    best = 0                  # 512 rows (profiles/r03/s5_m512/probe_*.jsonl: Llama-3 down 67 vs 93 us at 4 ranges)
     for s in range(1, K // 256 + 1):
         if K % (64 * s):
             continue
