@@ -107,27 +107,13 @@ _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "
 
 # kernels that own accumulator registers by name inside their inline asm (x64: O = a[0:127], Q = a[128:191];
 # x32: O = a[0:63], Q = a[64:95])
-ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernelILb0E", "prefill_x32_kernelILb1E")   # x32: one-shot, persistent
-# accumulator registers each kernel owns by name; the compiler may use the rest of the file (the persistent x32
-# spills a few loop-invariant lane values into a96 and up, outside its step loop)
-OWNED_AGPRS = {"prefill_x64_kernel": 192, "prefill_x32_kernelILb0E": 96, "prefill_x32_kernelILb1E": 96}
-
-
-def _agprs(text: str) -> set:
-    out = set()
-    for m in re.finditer(r"\ba\[(\d+):(\d+)\]|\ba(\d+)\b", text):
-        if m.group(3) is not None:
-            out.add(int(m.group(3)))
-        else:
-            out.update(range(int(m.group(1)), int(m.group(2)) + 1))
-    return out
+ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernel")
 
 
 def audit_x64(asm: str, kname: str = "prefill_x64_kernel") -> list:
     """prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]) inside its inline asm;
     hipcc knows nothing of that.  Returns the violations (empty = clean):
-      * any AGPR operand in the kernel's owned range (OWNED_AGPRS) that the COMPILER emitted (outside the kernel's
-        ;;#ASMSTART..;;#ASMEND blocks);
+      * any v_accvgpr_* / AGPR operand the COMPILER emitted (outside the kernel's ;;#ASMSTART..;;#ASMEND blocks);
       * any scratch traffic in the kernel;
       * an LDS-DMA whose descriptor SGPRs were written by a VALU op fewer than 5 wait states earlier (the kernel's
         DMA pieces after the first of a tile carry no s_nop of their own)."""
@@ -141,8 +127,7 @@ def audit_x64(asm: str, kname: str = "prefill_x64_kernel") -> list:
         elif t.startswith(";;#ASMEND"):
             inside = False
         elif t and not t.startswith((";", ".")) and not inside and ("accvgpr" in t or re.search(r"\ba\[?\d", t)):
-            if any(a < OWNED_AGPRS.get(kname, 256) for a in _agprs(t.split(";")[0])):
-                bad.append("compiler AGPR use: " + t)
+            bad.append("compiler AGPR use: " + t)
     if "scratch_" in body:
         bad.append(f"scratch traffic in {kname}")
     ins = [t.strip() for t in body.splitlines()]

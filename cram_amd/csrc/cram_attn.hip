@@ -27,7 +27,6 @@
 #include <stdint.h>
 #include <stdlib.h>
 
-#include <algorithm>
 #include <atomic>
 #include <mutex>
 
@@ -1040,8 +1039,7 @@ inline void knobs_init() {
   std::call_once(g_knob_once, [] {
     const char* e = getenv("CRAM_PREFILL_VARIANT");
     g_knob[CRAM_KNOB_PREFILL_VARIANT].store(
-        (e && (e[0] == '0' || e[0] == '3' || e[0] == '4' || e[0] == '5' || e[0] == '6' || e[0] == '7' || e[0] == '8'))
-            ? e[0] - '0'
+        (e && (e[0] == '0' || e[0] == '3' || e[0] == '4' || e[0] == '6' || e[0] == '7' || e[0] == '8')) ? e[0] - '0'
                                                                                                   : -1);
     const char* eu = getenv("CRAM_DECODE_U");
     g_knob[CRAM_KNOB_DECODE_U].store((eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1);
@@ -1054,19 +1052,6 @@ inline int knob(int k) {
   return g_knob[k].load(std::memory_order_relaxed);
 }
 
-// compute units of the current device (cached per device; the persistent prefill grid is two workgroups per CU)
-inline int num_cus() {
-  static std::atomic<int> cache[16];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
-  std::atomic<int>& c = cache[dev & 15];
-  int n = c.load(std::memory_order_relaxed);
-  if (n <= 0) {
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    c.store(n, std::memory_order_relaxed);
-  }
-  return n;
-}
 inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15u) == 0; }
 inline bool m8(int64_t s) { return (s & 7) == 0; }
 
@@ -1103,18 +1088,13 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // 1.16x at 8.3k tokens unbiased / biased (= x64 / 1.08x x64), 1.06x at B = 3 x 517 biased; 0.94x on a B = 2 x 77
   // call (tools/ab_x64.hip, profiles/r03/x32/)
   if constexpr (D == 128 && std::is_same<T, __bf16>::value) {
-    if ((kv == 4 || kv == 5 || (kv == -1 && p.Tq >= 256)) && G % 4 == 0) {
+    if ((kv == 4 || (kv == -1 && p.Tq >= 256)) && G % 4 == 0) {
       p.hp = 4;
       p.nqb = (p.Tq + 31) / 32;
       const int64_t nb = (int64_t)p.nqb * (p.Hq / 4) * p.B;
       if (nb > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
       p.nblocks = (int)nb;
-      if (kv == 5) {   // persistent form: two workgroups per CU walk the items (a multiple of 8: v & 7 = the XCD)
-        const int grid = std::min(p.nblocks, 2 * num_cus());
-        hipLaunchKernelGGL(prefill_x32_kernel<true>, dim3(grid), dim3(256), 0, stream, p);
-      } else {
-        hipLaunchKernelGGL(prefill_x32_kernel<false>, dim3(p.nblocks), dim3(256), 0, stream, p);
-      }
+      hipLaunchKernelGGL(prefill_x32_kernel, dim3(p.nblocks), dim3(256), 0, stream, p);
       return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
     }
   }
@@ -1218,8 +1198,8 @@ int cram_abi_version(void) { return CRAM_ABI_VERSION; }
 int cram_set_knob(int which, int value) {
   if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
   knobs_init();
-  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 4 && value != 5 &&
-      value != 6 && value != 7 && value != 8)
+  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 4 && value != 6 &&
+      value != 7 && value != 8)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;

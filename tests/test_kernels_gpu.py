@@ -369,47 +369,6 @@ def test_prefill_full_size_properties(gpu_device, prefill_variant, B, T):
             _check(oc[b, rows, h], ref)
 
 
-def test_persistent_x32_equals_one_shot(gpu_device):
-    """prefill_x32_kernel's persistent form (knob 5: 512 workgroups walk the blocks, the next block's Q / K(0) / V(0)
-    issued during the current one's last phases, V's ring parity carried over) computes every block with the one-shot
-    form's arithmetic: bit-identical outputs on the IE sweep's suffix call (biased heads, -inf and 0.1 spans, queries
-    after a 25-token prefix) and on a packed varlen call whose short sequences leave most blocks empty."""
-    from cram_amd import _lib, ops
-    dev = gpu_device
-    Hq, Hkv, d, B, T, p0 = 32, 8, 128, 33, 937, 25
-    g = torch.Generator(device=dev).manual_seed(5)
-    q = torch.randn(B, T, Hq, d, generator=g, device=dev).to(torch.bfloat16).transpose(1, 2)
-    k = torch.randn(B, Hkv, p0 + T, d, generator=g, device=dev).to(torch.bfloat16)
-    v = torch.randn(B, Hkv, p0 + T, d, generator=g, device=dev).to(torch.bfloat16)
-    w = torch.ones(B, p0 + T, dtype=torch.float16)
-    w[:, 30:200] = 0.0
-    w[:, 400:700] = 0.1
-    bias = hook_ref.log_weight(w).to(torch.bfloat16).float().to(dev)
-    enable = torch.zeros(B, Hq, dtype=torch.uint8, device=dev)
-    enable[:, ::3] = 1
-    lens = torch.randint(1, 1101, (48,), generator=torch.Generator().manual_seed(9)).tolist()
-    lens[5] = 1100
-    total = sum(lens)
-    qkv = torch.randn(total, (Hq + 2 * Hkv) * d, generator=g, device=dev).to(torch.bfloat16)
-    cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), dtype=torch.int32, device=dev)
-
-    def run():
-        a = ops.attn_prefill(q, k, v, scale=d ** -0.5, bias=bias, enable=enable, W=p0 + T - 3)
-        b = ops.attn_prefill_varlen(qkv[:, :Hq * d].view(total, Hq, d), qkv[:, Hq * d:(Hq + Hkv) * d].view(total, Hkv, d),
-                                    qkv[:, (Hq + Hkv) * d:].view(total, Hkv, d), cu, max(lens), scale=d ** -0.5)
-        return a, b
-    prev = _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, 4)
-    try:
-        one = run()
-        _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, 5)
-        per = run()
-    finally:
-        _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, prev)
-    torch.cuda.synchronize()
-    assert torch.equal(one[0], per[0])
-    assert torch.equal(one[1], per[1])
-
-
 def test_varlen_full_size_equals_dense(gpu_device, prefill_variant):
     """Config 2's packed prefill shape (64 prompts of 700-1100 tokens): every packed sequence equals its own
     dense single-sequence launch bit for bit (same tiles, same arithmetic)."""

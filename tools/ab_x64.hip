@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
       else if (which == 1)
         hipLaunchKernelGGL(prefill_x64_kernel, dim3(p2.nblocks), dim3(256), 0, 0, p2);
       else
-        hipLaunchKernelGGL(prefill_x32_kernel<false>, dim3(p3.nblocks), dim3(256), 0, 0, p3);
+        hipLaunchKernelGGL(prefill_x32_kernel, dim3(p3.nblocks), dim3(256), 0, 0, p3);
     };
     run(0);
     run(1);
