@@ -538,6 +538,7 @@ class DecodeSession:
         if Mp > total:
             h[total:].zero_()
         bias = self.cb.bias[b0:b1]
+        last = cu[1:].long() - 1                     # each sequence's last row: the only one the logits need
         m = None                                     # pending MLP output: layer output = h + m (add fused below)
         for l, lw in enumerate(eng.layers):
             if m is None:
@@ -552,6 +553,16 @@ class DecodeSession:
                            self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2), 0, pos=pos, dst_b=bidx,
                            keep_k=True)
             q = yr[:, :sp.q_size].view(total, sp.num_heads, sp.head_dim)
+            if l == sp.num_layers - 1:
+                # last layer: every row's K/V is in the cache now and only the last rows feed the logits, so their
+                # attention is one decode-kernel call over the cache and o_proj / MLP run on those rows alone (the
+                # other rows' last-layer outputs are never read: 2.7 % of the prefill's FLOPs)
+                a = ops.attn_decode(q[last], self.k_cache[l][b0:b1], self.v_cache[l][b0:b1], scale=eng.scale,
+                                    seq_lens=self.seq_lens[b0:b1], bias=bias, enable=self.cb.enable[l, b0:b1],
+                                    W=self.cb.W, num_splits=self.splits, workspace=self.ws)
+                h, x2 = ops.rmsnorm(ops.linear(a.flatten(-2), lw.wo), lw.ln2, sp.eps, residual=h[last])
+                m = eng.mlp(x2, lw)
+                break
             k = yr[:, sp.q_size:sp.q_size + sp.kv_size].view(total, sp.num_kv_heads, sp.head_dim)
             v = yr[:, sp.q_size + sp.kv_size:].view(total, sp.num_kv_heads, sp.head_dim)
             a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
@@ -562,8 +573,7 @@ class DecodeSession:
                                     out=a[:total].view(total, sp.num_heads, sp.head_dim))
             h, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
             m = eng.mlp(x2, lw)
-        last = cu[1:].long() - 1
-        _, hn = ops.rmsnorm(m[last], eng.norm, sp.eps, residual=h[last])
+        _, hn = ops.rmsnorm(m, eng.norm, sp.eps, residual=h)
         self.tokens[b0:b1] = self._pick(ops.linear(hn, eng.lm_head), slice(b0, b1))
 
     def _step_body(self):

@@ -13,6 +13,7 @@ head -c 300 $O/bench.json; echo
 mkdir -p $O/prof
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o sweep \
   -- python3 bench.py --no-cpu-baseline --no-decode > $O/prof/sweep.json 2> $O/prof/sweep.err
+python3 tools/trace_gaps.py $O/prof > $O/prof/gaps.txt 2>&1 || true
 find $O/prof -name "*kernel_trace.csv" -delete
 OUT=$O/pmc bash tools/pmc_attn.sh > $O/pmc_summary.txt 2>&1
 python3 tools/pmc_to_json.py $O/pmc > $O/attn_pmc.json
