@@ -592,8 +592,6 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
 #include "prefill_x64.inc"
 // two workgroups per CU, 32 rows per wave, the same hand-ordered stream: prefill_x32_kernel
 #include "prefill_x32.inc"
-// the same stream on v_mfma_f32_16x16x32 (knob value 5, opt-in): prefill_x16_kernel
-#include "prefill_x16.inc"
 
 // --------------------------------------------------------------------------------------------
 // decode (q_len == 1)
@@ -1041,8 +1039,7 @@ inline void knobs_init() {
   std::call_once(g_knob_once, [] {
     const char* e = getenv("CRAM_PREFILL_VARIANT");
     g_knob[CRAM_KNOB_PREFILL_VARIANT].store(
-        (e && (e[0] == '0' || e[0] == '3' || e[0] == '4' || e[0] == '5' || e[0] == '6' || e[0] == '7' || e[0] == '8'))
-            ? e[0] - '0'
+        (e && (e[0] == '0' || e[0] == '3' || e[0] == '4' || e[0] == '6' || e[0] == '7' || e[0] == '8')) ? e[0] - '0'
                                                                                                   : -1);
     const char* eu = getenv("CRAM_DECODE_U");
     g_knob[CRAM_KNOB_DECODE_U].store((eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1);
@@ -1091,15 +1088,6 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // 1.16x at 8.3k tokens unbiased / biased (= x64 / 1.08x x64), 1.06x at B = 3 x 517 biased; 0.94x on a B = 2 x 77
   // call (tools/ab_x64.hip, profiles/r03/x32/)
   if constexpr (D == 128 && std::is_same<T, __bf16>::value) {
-    if (kv == 5 && G % 4 == 0) {   // prefill_x16_kernel: x32 on 16x16x32 MFMAs (opt-in)
-      p.hp = 4;
-      p.nqb = (p.Tq + 31) / 32;
-      const int64_t nb = (int64_t)p.nqb * (p.Hq / 4) * p.B;
-      if (nb > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
-      p.nblocks = (int)nb;
-      hipLaunchKernelGGL(prefill_x16_kernel, dim3(p.nblocks), dim3(256), 0, stream, p);
-      return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
-    }
     if ((kv == 4 || (kv == -1 && p.Tq >= 256)) && G % 4 == 0) {
       p.hp = 4;
       p.nqb = (p.Tq + 31) / 32;
@@ -1210,8 +1198,8 @@ int cram_abi_version(void) { return CRAM_ABI_VERSION; }
 int cram_set_knob(int which, int value) {
   if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
   knobs_init();
-  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 4 && value != 5 &&
-      value != 6 && value != 7 && value != 8)
+  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 4 && value != 6 &&
+      value != 7 && value != 8)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;

@@ -86,7 +86,7 @@ def test_kernel_knobs_latch_without_gpu():
         os.environ["CRAM_DECODE_U"] = "4"            # the environment is not re-read after the first query
         assert _lib.get_knob(_lib.KNOB_DECODE_U) == 2
         with pytest.raises(RuntimeError):
-            _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, 2)
+            _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, 5)
         # an unknown knob is an error code distinct from every knob value (-1 = automatic is a value)
         v = ctypes.c_int(123)
         assert L.cram_get_knob(99, ctypes.byref(v)) == -1 and v.value == 123
