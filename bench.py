@@ -70,7 +70,7 @@ def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, i
     kern = ("decode_mfma_kernel (16x16x32 matrix cores, GQA group of %d)" % G if G >= 4 and sp.head_dim == 128
             else "decode_kernel (VALU)") + (" + decode_combine_kernel (split %d)" % sess.splits if sess.splits > 1 else "")
     res = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-           "frac": round(ach / PEAK_HBM_GBS, 4), "kernel": kern,
+           "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None, "kernel": kern,
            "avg_launch_ms": round(ms, 4), "bytes_per_launch": kv_bytes, "batch": sess.B, "splits": sess.splits,
            "note": "layer 0 of the decode leg's prefilled KV cache, timed apart from the decode leg"}
     del sess
@@ -151,7 +151,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    # NQ-1000 on one GPU = two batches of 500: 512 prompts per GPU share every decode step's 15 GB weight read (the M = 512
+    # max rows per decode batch.  NQ-1000 on one GPU = two batches of 500: 512 prompts per GPU share every decode step's 15 GB weight read (the M = 512
     # projections run near the matrix-core rate, M = 256 ones at 1.5-4 TB/s of weights); the KV cache of 512 rows is
     # 69 GB of the 288 GB (round 3: 72.4 vs 67.9 questions/s at 256 on one box, profiles/r03/s5_probe1/)
     ap.add_argument("--decode-batch", type=int, default=512)
@@ -162,6 +162,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefix-skip", action="store_true", help="recompute rows before the first biased key (A/B)")
     ap.add_argument("--cpu-units", type=int, default=8, help="IE units of the CPU baseline sample (>= 1)")
+    ap.add_argument("--cpu-decode-steps", type=int, default=8,
+                    help="decode steps of the CPU decode baseline's sample (0 = skip it); extrapolated to --decode-tokens")
+    ap.add_argument("--decode-questions", type=int, default=0,
+                    help="questions decoded once across the ranks (default: the whole 1000-question set; config 5: "
+                         "one KV-budget batch per GPU)")
     ap.add_argument("--blas", default="hipblaslt", choices=["hipblas", "hipblaslt"])
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPU) or gloo (rehearsal)")
     ap.add_argument("--model", default=None, choices=["llama3-8b", "qwen2-7b", "llama2-13b"],
@@ -277,7 +282,12 @@ def main():
         log(f"[rank {rank}] IE sweep: {units} units in {elapsed:.2f}s -> {ie['value']:.1f} heads/s")
 
     # ------------------------------------------------------------------ batched reweighted decode (configs 2, 4, 5)
+    # The question set is decoded exactly once across the ranks (cram_amd.dist.decode_sharded: LPT on prompt length,
+    # each rank's share in batches of at most --decode-batch rows, answers all-gathered), as RAG_test.py:64-176 answers
+    # every question once: NQ-1000 / TriviaQA-1000 for configs 2-4 (strong scaling over N), config 5 one KV-budget
+    # batch per GPU of long-context questions.
     decode = None
+    dec_cpu_input = None
     if not args.no_decode:
         if model == "qwen2-7b":
             heads, heads_desc = {}, "all heads (no Qwen2 head fixture)"
@@ -285,10 +295,14 @@ def main():
             key = "nq__llama2_13b_chat" if model == "llama2-13b" else "nq__llama3"
             heads = json.load(open(os.path.join(REPO, "data", "selected_heads.json")))[key]["heads"]
             heads_desc = f"{key} selected_heads top-{sum(len(v) for v in heads.values())}"
-        B = args.decode_batch if args.config != 5 else min(args.decode_batch, 16)
+        if args.config == 5:
+            # 20 retrieved docs (~8.3k tokens): rows per GPU from the KV budget (decode_batch, below), one batch each
+            nq_dec = args.decode_questions or world * args.decode_batch
+        else:
+            nq_dec = args.decode_questions or len(data)
+        nq_dec = min(nq_dec, len(data))
         qs, ps, ss = [], [], []
-        for j in range(B):
-            qi = (rank * B + j) % len(data)
+        for qi in range(nq_dec):
             rec = data[qi]
             if args.config == 5:
                 paras, sc = long_context_paras(data, qi)
@@ -302,20 +316,37 @@ def main():
         th = time.perf_counter()
         encs = spans.encode_batch(tok, name, qs, ps, ss)                     # host: prompts -> ids + fp16 weights
         host_ms = (time.perf_counter() - th) * 1e3
-        # the static KV cache is [L][B][Hkv][S_max][d] for K and V: MHA models (Llama-2-13b: 40 kv heads, 0.9 GB
-        # per 1.1k-token row) cap the batch at what fits next to the weights and the packed-prefill activations
-        s_max = max(ids.numel() for ids, _, _ in encs) + args.decode_tokens
+        lens = [ids.numel() for ids, _, _ in encs]
+        # the static KV cache is [L][B][Hkv][S_max][d] for K and V: rows per batch = what fits in 0.55 of HBM next
+        # to the weights and the packed-prefill activations (config 5: ~1.1 GB per 8.4k-token row -> ~128 rows;
+        # MHA Llama-2-13b: 0.9 GB per 1.1k-token row)
+        s_max = max(lens) + args.decode_tokens
         per_row = 2 * spec.num_layers * spec.num_kv_heads * s_max * spec.head_dim * 2
         cap = max(1, int(0.55 * torch.cuda.get_device_properties(dev).total_memory // per_row))
-        if cap < B:
-            log(f"[rank {rank}] decode batch {B} -> {cap} (KV cache {per_row / 2**20:.0f} MiB per row)")
-            B, encs = cap, encs[:cap]
-        prompts = [ids.to(dev) for ids, _, _ in encs]
+        B = min(args.decode_batch, cap)
+        if B < args.decode_batch:
+            log(f"[rank {rank}] decode batch {args.decode_batch} -> {B} (KV cache {per_row / 2**20:.0f} MiB per row)")
+        if args.config == 5 and not args.decode_questions:
+            nq_dec = min(len(data), world * B)
+            encs, lens = encs[:nq_dec], lens[:nq_dec]
+        prompts = [ids for ids, _, _ in encs]
         ws = [w for _, w, _ in encs]
-        # warm-up at the timed shape (the packed prefill's GEMM heuristics and buffers, the batch-B graph)
+        costs = [float(n) for n in lens]
+        gen_kw = dict(max_new_tokens=args.decode_tokens, eos_ids=(), use_graph=True, stop_on_eos=False)
+        my_batches = cdist.decode_batches(cdist.lpt_shards(costs, world)[rank], costs, B)
+        dev_prompts = {}
+
+        def dec_fn(idx, phases=None):
+            ps_ = [dev_prompts.setdefault(i, prompts[i].to(dev)) for i in idx]
+            if phases is not None:
+                phases.append({})
+            return eng.generate(ps_, [ws[i] for i in idx], heads, phases=phases[-1] if phases is not None else None,
+                                **gen_kw)
+
+        # warm-up at the timed shape (the packed prefill's GEMM heuristics and buffers, the batch graph)
         for _ in range(max(1, args.warmup)):
-            eng.generate(prompts, ws, heads, max_new_tokens=args.decode_tokens, eos_ids=(), use_graph=True,
-                         stop_on_eos=False)
+            if my_batches:
+                dec_fn(my_batches[0])
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -323,45 +354,86 @@ def main():
         phases = []
         td = time.perf_counter()
         for _ in range(reps):
-            phases.append({})
-            eng.generate(prompts, ws, heads, max_new_tokens=args.decode_tokens, eos_ids=(), use_graph=True,
-                         stop_on_eos=False, phases=phases[-1])
+            answers = cdist.decode_sharded(lambda idx: dec_fn(idx, phases), nq_dec, costs, B)
         torch.cuda.synchronize()
         dt = torch.tensor([time.perf_counter() - td], device=dev, dtype=torch.float64)
         if world > 1:
             dt = cdist.all_reduce_host(dt, "max")
-        T_mean = sum(p.numel() for p in prompts) / len(prompts)
-        decode = {"metric": "questions/sec reweighted-decode", "value": world * B * reps / float(dt.item()),
-                  "unit": "questions/s", "batch_per_gpu": B, "new_tokens": args.decode_tokens,
-                  "heads": heads_desc, "scores": ("GPT truthful, -min, /max, stable sort" if args.scores == "gpt" and dsname == "nq"
+        assert len(answers) == nq_dec and all(len(a) == args.decode_tokens for a in answers), "missing answers"
+        T_mean = sum(lens) / len(lens)
+        val = nq_dec * reps / float(dt.item())
+        decode = {"metric": "questions/sec reweighted-decode", "value": val, "unit": "questions/s",
+                  "questions": nq_dec, "each_question_once": True, "per_gpu": val / world,
+                  "scaling": "strong" if args.config != 5 else "weak",
+                  "batch_per_gpu": B, "batches_on_rank0": [len(b) for b in my_batches],
+                  "new_tokens": args.decode_tokens, "heads": heads_desc,
+                  "scores": ("GPT truthful, -min, /max, stable sort" if args.scores == "gpt" and dsname == "nq"
                              else "ideal: fake 0.1, others 1.0"), "mean_prompt_tokens": round(T_mean, 1),
                   "seconds": float(dt.item()), "repeats": reps,
-                  "host_encode_ms_per_question": round(host_ms / B, 3),
-                  "note": "packed varlen prefill + graph-replayed greedy steps, EOS ignored (random weights)"}
-        decode["leg_roofline"] = decode_leg_roofline(spec, phases, mdtype)
-        decode["attention_roofline"] = decode_attention_roofline(eng, prompts, ws, heads, args.decode_tokens, dev)
-        log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s (T mean {T_mean:.0f}); decode attention "
-            f"{decode['attention_roofline']['achieved']:.0f} GB/s")
+                  "host_encode_ms_per_question": round(host_ms / len(encs), 3),
+                  "note": (f"{nq_dec} {dsname} questions, each decoded once across {world} rank(s) "
+                           "(cram_amd.dist.decode_sharded: LPT on prompt length, batches of <= batch_per_gpu rows, "
+                           "answers all-gathered); packed varlen prefill + graph-replayed greedy steps, EOS ignored "
+                           "(random weights)")}
+        if phases:
+            decode["leg_roofline"] = decode_leg_roofline(spec, phases, mdtype)
+        if my_batches:
+            b0 = my_batches[0]
+            decode["attention_roofline"] = decode_attention_roofline(eng, [dev_prompts[i] for i in b0],
+                                                                     [ws[i] for i in b0], heads, args.decode_tokens,
+                                                                     dev)
+        # the CPU baseline's question: the one nearest the mean prompt length
+        qc = min(range(nq_dec), key=lambda i: (abs(lens[i] - T_mean), i))
+        dec_cpu_input = (qc, prompts[qc], ws[qc], heads)
+        log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s ({nq_dec} questions, T mean {T_mean:.0f}); "
+            f"decode attention {decode.get('attention_roofline', {}).get('achieved', 0):.0f} GB/s")
+        del dev_prompts
 
-    # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1, config 3)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and ie is not None:
+    # ------------------------------------------------------------------ CPU baselines (rank 0, N = 1)
+    # the reference's own algorithm on the host cores (oracle/cpu_baseline.py): IE units (config 3) and the hooked
+    # greedy decode of one question (configs 2-5), sampled and extrapolated, after the timed regions
+    cpu = cpu_dec = None
+    want_ie = ie is not None
+    want_dec = decode is not None and args.cpu_decode_steps > 0
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and (want_ie or want_dec):
         from oracle import cpu_baseline
         t0 = time.time()
         cpu_model = cpu_baseline.hf_model_from_engine(eng)
-        qi, ids, w, ans = ie["work"][0]
-        units_s = cpu_baseline.sample_units(L, H, max(1, args.cpu_units))
-        r = cpu_baseline.time_ie_units(cpu_model, ids.cpu(), w, ans.cpu(), units_s)
-        sp_ = r["spread"]
-        cpu = {"value": r["units_per_s"], "unit": "heads/s", "cores": r["cores"], "kind": "port",
-               "sample": f"{r['units']} IE units {units_s} over {len(set(l for l, _ in units_s))} layers (hooked full "
-                         f"forward + full-vocab logits + .item(), re_weighting.py:162-171) of NQ question {qi} at "
-                         f"T'={ids.numel()}, after 1 un-hooked forward; {r['seconds']:.1f}s; {result['dtype']} torch "
-                         f"CPU; extrapolates linearly per unit",
-               "unit_seconds": {"min": round(sp_["min_s"], 3), "median": round(sp_["median_s"], 3),
-                                "max": round(sp_["max_s"], 3)}}
+        log(f"[rank 0] CPU copy of the model in {time.time() - t0:.0f}s")
+        if want_ie:
+            qi, ids, w, ans = ie["work"][0]
+            units_s = cpu_baseline.sample_units(L, H, max(1, args.cpu_units))
+            r = cpu_baseline.time_ie_units(cpu_model, ids.cpu(), w, ans.cpu(), units_s)
+            sp_ = r["spread"]
+            cpu = {"value": r["units_per_s"], "unit": "heads/s", "cores": r["cores"], "kind": "port",
+                   "sample": f"{r['units']} IE units {units_s} over {len(set(l for l, _ in units_s))} layers (hooked "
+                             f"full forward + full-vocab logits + .item(), re_weighting.py:162-171) of NQ question {qi} "
+                             f"at T'={ids.numel()}, after 1 un-hooked forward; {r['seconds']:.1f}s; {result['dtype']} "
+                             f"torch CPU; extrapolates linearly per unit",
+                   "unit_seconds": {"min": round(sp_["min_s"], 3), "median": round(sp_["median_s"], 3),
+                                    "max": round(sp_["max_s"], 3)}}
+            log(f"[rank 0] cpu baseline {cpu['value']:.4f} heads/s on {cpu['cores']} cores")
+        if want_dec:
+            qc, ids, w, hd = dec_cpu_input
+            r = cpu_baseline.time_decode(cpu_model, ids.cpu(), w, hd if hd else
+                                         {l: list(range(H)) for l in range(L)},
+                                         new_tokens=args.decode_tokens, sampled_steps=args.cpu_decode_steps)
+            cpu_dec = {"value": r["questions_per_s"], "unit": "questions/s", "cores": r["cores"], "kind": "port",
+                       "method": "sampled + extrapolated",
+                       "sample": (f"1 question ({dsname} #{qc}, {r['prompt_tokens']} prompt tokens, {r['heads']} "
+                                  f"hooked heads): hooks on the selected heads + greedy generate "
+                                  f"(re_weighting.py:115-138) of 1 + {r['sampled_steps']} tokens, {r['seconds']:.1f}s; "
+                                  f"prefill {r['prefill_s']:.2f}s + {args.decode_tokens - 1} x median step "
+                                  f"{r['step_s']['median']:.3f}s = {r['question_s']:.1f}s per question at "
+                                  f"{args.decode_tokens} new tokens; {result['dtype']} torch CPU, batch 1 as the "
+                                  f"reference"),
+                       "prefill_s": round(r["prefill_s"], 3),
+                       "step_seconds": {k: round(v, 4) for k, v in r["step_s"].items()}}
+            decode["cpu_baseline"] = cpu_dec
+            decode["speedup_vs_cpu"] = round(decode["value"] / cpu_dec["value"], 1)
+            log(f"[rank 0] cpu decode baseline {cpu_dec['value']:.5f} questions/s on {cpu_dec['cores']} cores")
         del cpu_model
-        log(f"[rank 0] cpu baseline {cpu['value']:.4f} heads/s on {cpu['cores']} cores ({time.time() - t0:.0f}s)")
+        log(f"[rank 0] CPU baselines took {time.time() - t0:.0f}s")
 
     if rank == 0:
         if ie is not None:
@@ -388,6 +460,13 @@ def main():
                         roof["traffic_note"] = (f"HBM bytes/launch = PMC (FETCH_SIZEx2 + WRITE_SIZE, {pmc['source']}, "
                                                 f"kernel source {cur}) / algorithmic = {ratio:.4f} at the sweep shape "
                                                 f"B=33 T=962, x this run's algorithmic bytes per launch")
+                        # rocprofv3's own view of the same kernel (tools/pmc_to_json.py): MFMA utilisation and HBM
+                        # rate against the gfx950 peaks, at the sweep shape, from the PMC passes of this build
+                        roof["rocprof"] = {k: pmc[k] for k in (
+                            "mfma_busy", "effective_clock_ghz", "valu_per_mfma", "mfma_issues_over_algorithmic",
+                            "hbm_gbs", "hbm_frac", "tflops", "mfma_frac_of_peak", "avg_launch_ms_under_pmc",
+                            "wait_any_frac") if k in pmc}
+                        roof["mfma_busy"] = pmc.get("mfma_busy")
                     else:
                         roof["traffic_note"] = (f"PMC evidence {pmc['source']} was measured on kernel source "
                                                 f"{pmc.get('kernel_source_hash')}, this build is {cur}: not applied")
@@ -428,11 +507,16 @@ def main():
                   5: "Llama-3-8B NQ 20 retrieved docs (~8k tokens) reweighted decode (top-894 heads)"}[args.config]
             result.update({"metric": METRIC + f" [config {args.config}: decode]", "value": round(decode["value"], 3),
                            "unit": "questions/s", "ms_per_step": round(decode["seconds"] * 1e3 / decode["repeats"], 2),
-                           "scaling": "weak", "data": f"synthetic: random-init {model} weights; rebuilt {dsname} prompts",
-                           "config": {"workload": wl, "model": model, "batch_per_gpu": decode["batch_per_gpu"],
+                           "scaling": decode["scaling"],
+                           "data": f"synthetic: random-init {model} weights; rebuilt {dsname} prompts",
+                           "config": {"workload": wl, "model": model, "questions": decode["questions"],
+                                      "batch_per_gpu": decode["batch_per_gpu"],
                                       "new_tokens": decode["new_tokens"], "mean_prompt_tokens": decode["mean_prompt_tokens"],
-                                      "parallelism": f"dp{world} replicas (question-sharded)"},
-                           "roofline": None, "cpu_baseline": None, "decode": decode})
+                                      "parallelism": f"dp{world} replicas, each question decoded once "
+                                                     f"(cram_amd.dist.decode_sharded)"},
+                           "roofline": decode.get("attention_roofline"), "cpu_baseline": cpu_dec, "decode": decode})
+            if cpu_dec:
+                result["speedup_vs_cpu"] = decode["speedup_vs_cpu"]
         print(json.dumps(result), flush=True)
     if world > 1:
         torch.distributed.barrier()

@@ -29,23 +29,54 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the CrAM HIP library cannot be built")
 
 
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+HASH_TAG = b"CRAM_SOURCE_HASH="
+
+
+def source_hash() -> str:
+    """Identity of everything the library is built from: every source and header, the flags and the target."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in SOURCES + HEADERS:
+        h.update(f.name.encode() + b"\0" + f.read_bytes())
+    h.update(" ".join(COMMON_FLAGS + [ARCH]).encode())
+    return h.hexdigest()[:16]
+
+
+def built_hash(path: Path = LIB_PATH):
+    """The source hash a built library carries (cram_spans.cpp embeds "CRAM_SOURCE_HASH=<hash>"), or None."""
+    try:
+        data = path.read_bytes()
+    except OSError:
+        return None
+    i = data.find(HASH_TAG)
+    return data[i + len(HASH_TAG): i + len(HASH_TAG) + 16].decode("ascii", "replace") if i >= 0 else None
+
+
 def needs_build() -> bool:
-    if not LIB_PATH.exists():
-        return True
-    mtime = LIB_PATH.stat().st_mtime
-    return any(p.stat().st_mtime > mtime for p in SOURCES + HEADERS)
+    """True unless the installed library was built from exactly the current sources (by content hash, not mtime:
+    a snapshot copied with newer mtimes, or a library copied in with stale sources, is caught either way)."""
+    return built_hash() != source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile ``libcram_attn.so`` for gfx950 if it is missing or stale (one hipcc process per source, in
-    parallel, then one link)."""
-    if not force and not needs_build():
-        return LIB_PATH
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    """Compile ``libcram_attn.so`` for gfx950 if it is missing or built from other sources (one hipcc process per
+    source, in parallel, then one link).  Concurrent builds (two test sessions) serialise on a lock file."""
+    import fcntl
     objdir = PKG_DIR / "build"
     objdir.mkdir(exist_ok=True)
-    common = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-              "-I", str(REPO_DIR / "include")]
+    with open(objdir / ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and not needs_build():
+            return LIB_PATH
+        return _build(objdir, verbose)
+
+
+def _build(objdir: Path, verbose: bool) -> Path:
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    sh = source_hash()
+    common = [_hipcc(), f"--offload-arch={ARCH}", *COMMON_FLAGS, "-I", str(REPO_DIR / "include"),
+              f'-DCRAM_SOURCE_HASH="{sh}"']
     objs, procs = [], []
     for src in SOURCES:
         obj = objdir / (src.name + ".o")
@@ -61,20 +92,36 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         raise subprocess.CalledProcessError(1, failed[0])
     asm = x64_asm_path().read_text()
     for kname in ASM_KERNELS:
-        bad = audit_x64(asm, kname)
+        bad = audit_asm_kernel(asm, kname)
         if bad:
             raise RuntimeError(f"{kname} register audit failed (the library is not installed): " + "; ".join(bad[:5]))
+    (objdir / "asm.hash").write_text(sh)
     link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(tmp)]
     if verbose:
         print(" ".join(link), file=sys.stderr)
     subprocess.run(link, check=True)
+    if built_hash(tmp) != sh:
+        raise RuntimeError("the linked library does not carry its source hash (cram_spans.cpp tag missing)")
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 
+def device_asm(out_dir: Path) -> str:
+    """Device assembly of cram_attn.hip compiled with the library's flags into out_dir (for the register audit
+    without touching the installed library): the saved assembly of the last build when it matches the sources."""
+    saved, stamp = x64_asm_path(), PKG_DIR / "build" / "asm.hash"
+    if saved.exists() and stamp.exists() and stamp.read_text().strip() == source_hash():
+        return saved.read_text()
+    out = Path(out_dir) / "cram_attn.s"
+    subprocess.run([_hipcc(), f"--offload-arch={ARCH}", *COMMON_FLAGS, "-I", str(REPO_DIR / "include"),
+                    "--cuda-device-only", "-S", str(CSRC / "cram_attn.hip"), "-o", str(out)], check=True)
+    return out.read_text()
+
+
 def kernel_source_hash() -> str:
-    """Identity of the attention kernels' source (cram_attn.hip, prefill_x64.inc, the ABI header): PMC evidence
-    (profiles/attn_pmc.json) records the hash it was measured on, and bench.py uses it only while it matches."""
+    """Identity of the attention kernels' source (cram_attn.hip, prefill_x64.inc, prefill_x32.inc, the ABI header):
+    PMC evidence (profiles/attn_pmc.json) records the hash it was measured on, and bench.py uses it only while it
+    matches."""
     import hashlib
     h = hashlib.sha256()
     for f in (CSRC / "cram_attn.hip", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc", REPO_DIR / "include" / "cram_attn.h"):
@@ -110,9 +157,10 @@ _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "
 ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernel")
 
 
-def audit_x64(asm: str, kname: str = "prefill_x64_kernel") -> list:
-    """prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]) inside its inline asm;
-    hipcc knows nothing of that.  Returns the violations (empty = clean):
+def audit_asm_kernel(asm: str, kname: str = "prefill_x32_kernel") -> list:
+    """The kernels of ASM_KERNELS own accumulator registers by name inside their inline asm (prefill_x64_kernel:
+    O = a[0:127], Q = a[128:191]; prefill_x32_kernel: O = a[0:63], Q = a[64:95]); hipcc knows nothing of that.
+    Returns the violations in kernel `kname` (empty = clean):
       * any v_accvgpr_* / AGPR operand the COMPILER emitted (outside the kernel's ;;#ASMSTART..;;#ASMEND blocks);
       * any scratch traffic in the kernel;
       * an LDS-DMA whose descriptor SGPRs were written by a VALU op fewer than 5 wait states earlier (the kernel's
@@ -151,6 +199,9 @@ def audit_x64(asm: str, kname: str = "prefill_x64_kernel") -> list:
     if n_dma == 0:
         bad.append("no LDS-DMA without its own s_nop found: the audit no longer matches the kernel")
     return bad
+
+
+audit_x64 = audit_asm_kernel          # the round-2 name (x64 was the first such kernel)
 
 
 if __name__ == "__main__":

@@ -12,6 +12,13 @@
 
 #include "cram_attn.h"
 
+// The build's source hash (cram_amd/build.py: sha256 of every source, header and flag), embedded as a tag the
+// Python side reads from the .so file itself, so a stale library is rebuilt by content, never by mtime.
+#ifdef CRAM_SOURCE_HASH
+extern "C" __attribute__((used, visibility("default"))) const char cram_source_hash_tag[] =
+    "CRAM_SOURCE_HASH=" CRAM_SOURCE_HASH;
+#endif
+
 namespace {
 
 uint16_t f32_to_f16_bits(float f) {

@@ -18,8 +18,12 @@ appends one JSON line per finished (question, layer) to its own file
 identity (a hash of question, passages, scores and wrong answer) and a run
 fingerprint (model, shapes, logit convention); a restarted run — any world size,
 any order or subset of questions — reads every shard file, skips the units whose
-(identity, layer) is already there and fills them from disk.  Decode is replica-only (question-sharded,
-no collective).
+(identity, layer) is already there and fills them from disk.
+
+Decode (replicas only, question-sharded): `decode_sharded` deals a question list over the ranks by
+LPT on prompt length, each rank decodes its share in batches of at most `batch` rows, and the answers meet on
+every rank through one `all_gather_object` (with per-rank answer files, resumable by question identity).  Every
+question is answered exactly once across ranks, as RAG_test.py:64-176 answers each question once.
 """
 from __future__ import annotations
 
@@ -140,11 +144,15 @@ def unit_key(*parts) -> str:
     return hashlib.sha256(json.dumps(parts, ensure_ascii=False, sort_keys=True).encode("utf-8")).hexdigest()[:24]
 
 
-def read_shards(shard_dir: str, num_heads: int, run: str = "") -> Dict[Tuple[str, int], List[float]]:
+def read_shards(shard_dir: str, num_heads: int, run: str = "",
+                log: Optional[Callable[[str], None]] = None) -> Dict[Tuple[str, int], List[float]]:
     """{(question key, layer): IE row} from every rank's append-only file, restricted to records of this run
     fingerprint (model, layer / head counts, logit convention); a torn line (a killed writer) is ignored, a later
-    line for the same unit wins."""
+    line for the same unit wins.  Records that are skipped for another reason — written by the pre-identity format
+    ({q, layer, ie} without a key), by another run fingerprint or with another head count — are counted and
+    reported through `log` (default: a warning on stderr), so a resume that recomputes everything says why."""
     done: Dict[Tuple[str, int], List[float]] = {}
+    skipped = {"no key (old format)": 0, "other run": 0, "other head count": 0}
     for fn in sorted(glob.glob(os.path.join(shard_dir, "rank*.jsonl"))):
         with open(fn, encoding="utf-8") as f:
             for line in f:
@@ -152,9 +160,24 @@ def read_shards(shard_dir: str, num_heads: int, run: str = "") -> Dict[Tuple[str
                     rec = json.loads(line)
                 except ValueError:
                     continue
-                if (isinstance(rec, dict) and isinstance(rec.get("key"), str) and rec.get("run", "") == run
-                        and len(rec.get("ie", ())) == num_heads):
+                if not isinstance(rec, dict):
+                    continue
+                if not isinstance(rec.get("key"), str):
+                    skipped["no key (old format)"] += 1
+                elif rec.get("run", "") != run:
+                    skipped["other run"] += 1
+                elif len(rec.get("ie", ())) != num_heads:
+                    skipped["other head count"] += 1
+                else:
                     done[(rec["key"], int(rec["layer"]))] = [float(x) for x in rec["ie"]]
+    if any(skipped.values()):
+        msg = (f"cram_amd.dist: {shard_dir}: ignored checkpoint records ("
+               + ", ".join(f"{k}: {v}" for k, v in skipped.items() if v) + f"); reusing {len(done)}")
+        if log is not None:
+            log(msg)
+        else:
+            import sys
+            print("warning: " + msg, file=sys.stderr, flush=True)
     return done
 
 
@@ -204,7 +227,7 @@ def sweep_sharded(fn: Callable[[int, List[int]], torch.Tensor], n_questions: int
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if shard_dir and (keys is None or len(keys) != n_questions):
         raise ValueError("checkpointing needs one identity key per question (cram_amd.dist.unit_key)")
-    done = read_shards(shard_dir, num_heads, run) if shard_dir else {}
+    done = read_shards(shard_dir, num_heads, run, log) if shard_dir else {}
     if shard_dir and world > 1:
         dist.barrier(group)                   # every rank has read the same files before anyone appends
     writer = ShardWriter(shard_dir, rank, keys, run) if shard_dir else None
@@ -229,3 +252,107 @@ def sweep_sharded(fn: Callable[[int, List[int]], torch.Tensor], n_questions: int
                 if row is not None:
                     out[q * num_layers + l] = torch.tensor(row, dtype=torch.float32, device=out.device)
     return out.view(n_questions, num_layers, num_heads)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# question-sharded decode (SURVEY §8e "replicas only"; RAG_test.py:64-176 answers every question once)
+# ---------------------------------------------------------------------------------------------------------------
+def decode_batches(items: Sequence[int], costs: Sequence[float], batch: int) -> List[List[int]]:
+    """One rank's questions as decode batches of at most `batch` rows: sorted by cost (prompt length), so a batch's
+    rows have similar lengths (tight S_max, even per-row work), cut into ceil(n / batch) batches of near-equal size
+    (1000 questions at 512 rows -> 500 + 500, not 512 + 488)."""
+    if batch < 1:
+        raise ValueError("batch must be >= 1")
+    order = sorted(items, key=lambda i: (costs[i], i))
+    if not order:
+        return []
+    nb = -(-len(order) // batch)
+    base, extra = divmod(len(order), nb)
+    out, i = [], 0
+    for b in range(nb):
+        n = base + (1 if b < extra else 0)
+        out.append(order[i:i + n])
+        i += n
+    return out
+
+
+def read_answers(shard_dir: str, run: str = "") -> Dict[str, object]:
+    """{question key: answer} from every rank's append-only decode file `answers{r}.jsonl` (this run only; a torn
+    line is ignored)."""
+    done: Dict[str, object] = {}
+    for fn in sorted(glob.glob(os.path.join(shard_dir, "answers*.jsonl"))):
+        with open(fn, encoding="utf-8") as f:
+            for line in f:
+                try:
+                    rec = json.loads(line)
+                except ValueError:
+                    continue
+                if isinstance(rec, dict) and isinstance(rec.get("key"), str) and rec.get("run", "") == run:
+                    done[rec["key"]] = rec["answer"]
+    return done
+
+
+def _append_answers(path: str, recs: Sequence[dict]) -> None:
+    if os.path.exists(path) and os.path.getsize(path) > 0:          # end a torn line of a killed writer
+        with open(path, "rb+") as f:
+            f.seek(-1, os.SEEK_END)
+            if f.read(1) != b"\n":
+                f.write(b"\n")
+    with open(path, "a", encoding="utf-8") as f:
+        f.write("".join(json.dumps(r, ensure_ascii=False) + "\n" for r in recs))
+        f.flush()
+        os.fsync(f.fileno())
+
+
+def decode_sharded(fn: Callable[[List[int]], Sequence[object]], n_questions: int, costs: Sequence[float],
+                   batch: int, group=None, shard_dir: Optional[str] = None, keys: Optional[Sequence[str]] = None,
+                   run: str = "", log: Optional[Callable[[str], None]] = None) -> List[object]:
+    """Answers of n_questions questions, every question decoded exactly once across the ranks; the full list
+    (index order) is returned on every rank.
+
+    fn(indices) -> one answer per index (JSON-serialisable: generated ids, or (prompt, answer) strings): the batched
+    engine decode of those questions (CrAMEngine.generate / Re_Weighting_Strategy.run_RAG_batch).  Questions go to
+    ranks by LPT on `costs` (prompt tokens: a row's decode work grows with its length), each rank runs its share in
+    decode_batches of at most `batch` rows, and one all_gather_object assembles the answers.  With shard_dir every
+    rank appends its answers to answers{rank}.jsonl under the question identity keys[i]; a restarted run (any world
+    size, any order) decodes only the questions not on file for the same run fingerprint."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if shard_dir and (keys is None or len(keys) != n_questions):
+        raise ValueError("answer files need one identity key per question (cram_amd.dist.unit_key)")
+    done = read_answers(shard_dir, run) if shard_dir else {}
+    if shard_dir:
+        os.makedirs(shard_dir, exist_ok=True)
+        if world > 1:
+            dist.barrier(group)               # every rank has read the same files before anyone appends
+    mine = [i for i in lpt_shards(costs, world)[rank] if not (shard_dir and keys[i] in done)]
+    local: Dict[int, object] = {}
+    for chunk in decode_batches(mine, costs, batch):
+        ans = list(fn(list(chunk)))
+        if len(ans) != len(chunk):
+            raise RuntimeError(f"decode fn returned {len(ans)} answers for {len(chunk)} questions")
+        local.update(zip(chunk, ans))
+        if shard_dir:
+            _append_answers(os.path.join(shard_dir, f"answers{rank}.jsonl"),
+                            [{"key": keys[i], "run": run, "q": int(i), "answer": a} for i, a in zip(chunk, ans)])
+        if log is not None:
+            log(f"[rank {rank}] decoded {len(chunk)} questions ({len(local)}/{len(mine)})")
+    if world > 1:
+        parts: List[Optional[Dict[int, object]]] = [None] * world
+        dist.all_gather_object(parts, local, group=group)
+    else:
+        parts = [local]
+    out: List[object] = [None] * n_questions
+    seen = 0
+    for p in parts:
+        for i, a in (p or {}).items():
+            out[int(i)] = a
+            seen += 1
+    if shard_dir:
+        for i in range(n_questions):
+            if keys[i] in done and out[i] is None:
+                out[i] = done[keys[i]]
+                seen += 1
+    if seen != n_questions:
+        raise RuntimeError(f"decode_sharded: {seen} answers for {n_questions} questions")
+    return out

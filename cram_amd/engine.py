@@ -421,6 +421,13 @@ def decode_splits(N: int, K: int, rows: int) -> int:
     return best
 
 
+def decode_attn_splits(B: int, num_kv_heads: int, S_max: int) -> int:
+    """Split-S count of the decode attention: enough (batch row, kv head) work items x splits to cover ~512
+    workgroups, at most 16 splits and at least 256 keys per split."""
+    splits = max(1, min(16, math.ceil(512 / max(1, B * num_kv_heads))))
+    return max(1, min(splits, S_max // 256))
+
+
 class DecodeSession:
     """Static-shape state of one batched greedy decode (KV cache, bias, token buffers)."""
 
@@ -456,8 +463,7 @@ class DecodeSession:
             self.seen = torch.zeros((self.B, eng.lm_head.shape[0]), dtype=torch.bool, device=dev)
             for b, p in enumerate(self.prompts):
                 self.seen[b, p] = True
-        splits = max(1, min(16, math.ceil(512 / max(1, self.B * sp.num_kv_heads))))
-        self.splits = max(1, min(splits, self.S_max // 256))
+        self.splits = decode_attn_splits(self.B, sp.num_kv_heads, self.S_max)
         self.ws = (torch.empty(ops.decode_workspace_bytes(self.B, sp.num_heads, sp.head_dim, self.splits),
                                dtype=torch.uint8, device=dev) if self.splits > 1 else None)
         self.graph = None

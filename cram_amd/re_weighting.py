@@ -182,6 +182,26 @@ class Re_Weighting_Strategy:
             res.append((prompt, out[out.find(prompt) + len(prompt):]))
         return res
 
+    @torch.no_grad()
+    def run_RAG_sharded(self, questions: List[str], paras_list: List[list], scores_list: List[list],
+                        batch: int = 512, max_new_tokens: int = 100, shard_dir: Optional[str] = None,
+                        group=None) -> List[tuple]:
+        """(prompt, answer) of every question, each decoded exactly once across the ranks of the process group
+        (RAG_test.py:64-176 loops over the dataset once): questions dealt to ranks by LPT on prompt length,
+        run_RAG_batch on each rank's share in batches of at most `batch` rows, answers gathered on every rank
+        (cram_amd.dist.decode_sharded); with shard_dir, answers are checkpointed per rank and a restart resumes."""
+        from . import dist as _dist
+        costs = [float(len(q) + sum(len(x) for x in p)) for q, p in zip(questions, paras_list)]
+        keys = [_dist.unit_key(q, list(p), [float(x) for x in s]) for q, p, s in zip(questions, paras_list, scores_list)]
+        run = (f"decode|{self.model_name}|{str(self.model.dtype).replace('torch.', '')}|new={int(max_new_tokens)}|"
+               f"heads={_dist.unit_key(sorted((str(k), list(v)) for k, v in self.layers_to_be_modified.items()))}")
+
+        def fn(idx):
+            return [list(x) for x in self.run_RAG_batch([questions[i] for i in idx], [paras_list[i] for i in idx],
+                                                        [scores_list[i] for i in idx], max_new_tokens=max_new_tokens)]
+        return [tuple(a) for a in _dist.decode_sharded(fn, len(questions), costs, batch, group=group,
+                                                        shard_dir=shard_dir, keys=keys, run=run)]
+
 
 class Find_Best_Heads(Re_Weighting_Strategy):
     """re_weighting.py:141-175."""

@@ -1,10 +1,14 @@
 """ORACLE — test infrastructure only.  The timed CPU baseline of bench.py.
 
-The reference's IE sweep on the host cores (re_weighting.py:152-175): a
-transformers Llama model on the CPU, the restated dense-mask forward-pre-hook
-(oracle.hook_ref), one full forward with full-vocab logits per (layer, head)
-unit and a .item() per unit.  Weights are copied from the GPU engine so both
-sides run the same network.  Only bench.py's cpu_baseline leg calls this.
+Both halves of the metric on the host cores, through the reference's own
+algorithm: a transformers Llama / Qwen2 model on the CPU with the restated
+dense-mask forward-pre-hook (oracle.hook_ref):
+  * IE sweep (re_weighting.py:152-175): one full forward with full-vocab logits
+    per (layer, head) unit and a .item() per unit;
+  * reweighted decode (re_weighting.py:115-138): hooks on the selected heads,
+    then greedy `generate` at batch 1.
+Weights are copied from the GPU engine so both sides run the same network.
+Only bench.py's cpu_baseline legs call this.
 """
 from __future__ import annotations
 
@@ -17,19 +21,26 @@ from . import hook_ref
 
 
 def hf_model_from_engine(eng, rope_theta: float = 500000.0):
-    """A transformers LlamaForCausalLM on the CPU holding the engine's weights (in the engine's dtype)."""
-    from transformers import LlamaConfig, LlamaForCausalLM
+    """A transformers LlamaForCausalLM (Qwen2ForCausalLM for the qwen2 family, q/k/v biases included) on the CPU
+    holding the engine's weights (in the engine's dtype).  The rotary table is copied from the engine, so
+    rope_theta only fills the config."""
     sp = eng.spec
-    cfg = LlamaConfig(vocab_size=sp.vocab, hidden_size=sp.hidden, intermediate_size=sp.intermediate,
-                      num_hidden_layers=sp.num_layers, num_attention_heads=sp.num_heads,
-                      num_key_value_heads=sp.num_kv_heads, head_dim=sp.head_dim, rms_norm_eps=sp.eps,
-                      rope_theta=rope_theta, max_position_embeddings=8192, tie_word_embeddings=False)
+    common = dict(vocab_size=sp.vocab, hidden_size=sp.hidden, intermediate_size=sp.intermediate,
+                  num_hidden_layers=sp.num_layers, num_attention_heads=sp.num_heads,
+                  num_key_value_heads=sp.num_kv_heads, head_dim=sp.head_dim, rms_norm_eps=sp.eps, rope_theta=rope_theta,
+                  max_position_embeddings=16384, tie_word_embeddings=False)
+    if sp.family == "qwen2":
+        from transformers import Qwen2Config as Cfg, Qwen2ForCausalLM as Model
+        cfg = Cfg(**common)
+    else:
+        from transformers import LlamaConfig as Cfg, LlamaForCausalLM as Model
+        cfg = Cfg(**common)
     cfg._attn_implementation = "sdpa"
     prev = torch.get_default_dtype()
     torch.set_default_dtype(eng.dtype)
     try:
         with torch.device("meta"):
-            model = LlamaForCausalLM(cfg)
+            model = Model(cfg)
     finally:
         torch.set_default_dtype(prev)
     model = model.to_empty(device="cpu")
@@ -43,6 +54,11 @@ def hf_model_from_engine(eng, rope_theta: float = 500000.0):
             blk.self_attn.q_proj.weight.copy_(wqkv[:q])
             blk.self_attn.k_proj.weight.copy_(wqkv[q:q + kv])
             blk.self_attn.v_proj.weight.copy_(wqkv[q + kv:])
+            if lw.bqkv is not None:
+                b = lw.bqkv.cpu()
+                blk.self_attn.q_proj.bias.copy_(b[:q])
+                blk.self_attn.k_proj.bias.copy_(b[q:q + kv])
+                blk.self_attn.v_proj.bias.copy_(b[q + kv:])
             blk.self_attn.o_proj.weight.copy_(lw.wo.cpu())
             wgu = lw.wgu.cpu()
             blk.mlp.gate_proj.weight.copy_(wgu[:sp.intermediate])
@@ -101,3 +117,44 @@ def sample_units(num_layers: int, num_heads: int, n: int):
         l = round(fr[i % len(fr)] * (num_layers - 1)) if i < len(fr) else (i * 7) % num_layers
         out.append((int(l), int((i * 11 + 3) % num_heads)))
     return out
+
+
+@torch.no_grad()
+def time_decode(model, ids: torch.Tensor, w16: torch.Tensor, layers_to_heads: dict, new_tokens: int = 100,
+                sampled_steps: int = 8) -> dict:
+    """The reference's reweighted decode of one question on the CPU (re_weighting.py:115-138): forward-pre-hooks
+    on the selected heads (:118-124), greedy `generate` (:127-132).  Bounded sample: generate runs 1 + sampled_steps
+    tokens (min_new_tokens keeps EOS from ending it early); a StoppingCriteria stamps the clock after every token,
+    so the first stamp closes the prefill (+ the first token) and the rest are the per-token decode steps.  One
+    question's time at `new_tokens` = prefill + (new_tokens - 1) x median step (linear extrapolation; the per-step
+    attention cost grows by ~1 key per step, < 0.1 % of a ~900-token prompt's)."""
+    from transformers import StoppingCriteria, StoppingCriteriaList
+    torch.set_num_threads(cores())
+    ids = ids.reshape(1, -1).cpu()
+    lw = hook_ref.log_weight(w16.reshape(1, -1).cpu())
+    stamps = []
+
+    class _Stamp(StoppingCriteria):
+        def __call__(self, input_ids, scores, **kwargs):
+            stamps.append(time.perf_counter())
+            return torch.zeros(input_ids.shape[0], dtype=torch.bool)
+
+    n = 1 + max(1, int(sampled_steps))
+    hs = hook_ref.register_hooks(model, layers_to_heads, lw)
+    try:
+        t0 = time.perf_counter()
+        out = model.generate(input_ids=ids, attention_mask=torch.ones_like(ids), do_sample=False, max_new_tokens=n,
+                             min_new_tokens=n, stopping_criteria=StoppingCriteriaList([_Stamp()]), pad_token_id=0)
+    finally:
+        for h in hs:
+            h.remove()
+    if len(stamps) != n or out.shape[1] != ids.shape[1] + n:
+        raise RuntimeError(f"CPU decode sample produced {out.shape[1] - ids.shape[1]} tokens, {len(stamps)} stamps")
+    prefill = stamps[0] - t0
+    steps = sorted(b - a for a, b in zip(stamps, stamps[1:]))
+    med = steps[len(steps) // 2]
+    per_q = prefill + (max(1, int(new_tokens)) - 1) * med
+    return {"prefill_s": prefill, "step_s": {"min": steps[0], "median": med, "max": steps[-1]},
+            "sampled_steps": len(steps), "seconds": stamps[-1] - t0, "question_s": per_q,
+            "questions_per_s": 1.0 / per_q, "cores": cores(), "prompt_tokens": int(ids.shape[1]),
+            "heads": sum(len(v) for v in layers_to_heads.values())}

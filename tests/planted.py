@@ -37,8 +37,12 @@ from typing import List, Sequence, Tuple
 import numpy as np
 import torch
 
-# Llama-3-8B default: 130 pairs in tiers (count, largest target, smallest target) -> boundaries 10, 50, 100, 130, 894
-TIERS_LLAMA3 = ((10, 16.0, 12.0), (40, 8.0, 6.0), (50, 4.0, 3.0), (30, 2.0, 1.6))
+# Llama-3-8B default: 130 pairs in tiers (count, largest target, smallest target) -> boundaries 10, 50, 100, 130, 894.
+# Round 4: every designed boundary gap >= 1.8 (round 3: 0.99 at k = 100, 1.26 / 1.34 at 130 / 894
+# against a 3 x noise bar of 1.13), i.e. >= 1.5 x the bar at round 3's noise: tier edges 10.5 | 8.5, 7.0 | 5.0,
+# 4.5 | 2.6, and the last tier's 2.3 against random heads of |IE| <= 0.34; the top target drops 16 -> 12, which also
+# shrinks the bf16 noise of the largest IEs.
+TIERS_LLAMA3 = ((10, 12.0, 10.5), (40, 8.5, 7.0), (50, 5.0, 4.5), (30, 2.6, 2.3))
 
 
 @dataclass

@@ -4,8 +4,10 @@ depth is irrelevant to the kernels, the widths are not) — on one rebuilt Trivi
 [0.1, 1, 1, 1, 1] re-ordered as RAG_test.py:64-107 orders them, all heads re-weighted: layers_to_be_modified = {}).
 
 Pins the automatic GQA-7 choices together at the config's shape: the 7-wave prefill workgroups (hp7, <= 2048 tokens),
-the matrix-core decode for 7-head groups, the q/k/v bias in both the library GEMMs and the decode step's split-K
-GEMM (bias added in its combine), against
+the matrix-core decode for 7-head groups and the decode step's split-K down projection (the engine's rule routes only
+long-K projections through cram_gemm_splitk: at this shape K = 3584 < 2N for q/k/v, so the q/k/v bias runs in the
+library GEMM), and — with CRAM_DECODE_GEMM=all, which routes every decode projection through the split-K kernel — the
+q/k/v bias added in the split-K combine, against
   * the transformers drop-in on the same kernels (greedy ids up to the first near-tie, re_weighting.py:127-132);
   * the reference hook itself (oracle/hook_ref.py, dense mask, bf16 transformers) and the float32 truth (same hook
     on the float32 copy of the weights): re-weighted answer log-probs of the drop-in and of the engine within
@@ -59,11 +61,19 @@ def test_config4_shape_selects_the_gqa7_kernels(qwen7):
     assert 700 < enc["input_ids"].shape[1] < 1200
 
 
-def test_config4_engine_decode_matches_dropin(qwen7):
-    """run_RAG_batch (engine: packed varlen prefill, graph-replayed steps, split-K decode projections with the q/k/v
-    bias) == the transformers drop-in's model.generate on the cram_hip kernels, up to the first near-tie."""
+@pytest.mark.parametrize("decode_gemm", ["rule", "all"])
+def test_config4_engine_decode_matches_dropin(qwen7, decode_gemm, monkeypatch):
+    """run_RAG_batch (engine: packed varlen prefill, graph-replayed steps, split-K decode projections — by the
+    engine's rule, or all of them including the biased q/k/v with CRAM_DECODE_GEMM=all) == the transformers
+    drop-in's model.generate on the cram_hip kernels, up to the first near-tie."""
     from cram_amd import attention as A
+    from cram_amd.engine import DecodeSession
+    if decode_gemm == "all":
+        monkeypatch.setenv("CRAM_DECODE_GEMM", "all")
     obj, _, recs = qwen7
+    sk = DecodeSession(obj.engine, [torch.zeros(900, dtype=torch.long)] * 2, [torch.ones(1, 900, dtype=torch.float16)] * 2,
+                       {}, 4).splits_gemm
+    assert (sk["qkv"] > 0) == (decode_gemm == "all") and sk["down"] > 0, sk
     heads = obj.layers_to_be_modified
     qs, ps, ss = [r[0]["question"] for r in recs], [r[1] for r in recs], [r[2] for r in recs]
     batched = obj.run_RAG_batch(qs, ps, ss, max_new_tokens=16, use_graph=True)

@@ -212,3 +212,118 @@ def test_resume_after_kill(tmp_path, single):
     assert not redone & set(done), "a unit on disk was recomputed"
     assert len(redone) + len(done) == NQ * one.shape[1]
     assert len(cdist.read_shards(shards, one.shape[2])) == NQ * one.shape[1]
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# question-sharded decode (replicas only; RAG_test.py:64-176 answers every question exactly once)
+# ---------------------------------------------------------------------------------------------------------------
+NDEC = 6
+DEC_HEADS = {0: [1, 2], 2: [0], 3: [3]}
+DEC_LENS = (200, 137, 171, 150, 188, 120)
+
+
+def test_decode_batches_balance():
+    costs = [float(c) for c in (5, 1, 9, 3, 7, 2, 8)]
+    b = cdist.decode_batches(range(7), costs, 3)
+    assert [len(x) for x in b] == [3, 2, 2]                      # ceil(7 / 3) = 3 near-equal batches
+    assert [i for x in b for i in x] == sorted(range(7), key=lambda i: costs[i])
+    assert cdist.decode_batches([], costs, 4) == []
+    assert [len(x) for x in cdist.decode_batches(range(1000), [1.0] * 1000, 512)] == [500, 500]
+
+
+def _dec_inputs(path):
+    from transformers import AutoTokenizer
+    from cram_amd import spans
+    from tests import tiny_models as tm
+    tok = AutoTokenizer.from_pretrained(path)
+    with gzip.open(os.path.join(tm.REPO, "data", "nq_1000.json.gz"), "rt") as f:
+        nq = json.load(f)[:NDEC]
+    out = []
+    for rec, L in zip(nq, DEC_LENS):
+        _, enc, wt, _ = spans.encode(tok, path, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
+                                     [0.1, 1, 1, 1, 1], "")
+        out.append((enc["input_ids"][0, :L], wt[:, :L]))
+    return out
+
+
+def _dec_worker(rank, world, port, root, out_path, shard_dir, die_after):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from transformers import AutoModelForCausalLM
+    from cram_amd.engine import CrAMEngine
+    from tests import cpu_ops
+    from tests import tiny_models as tm
+    cdist.init("gloo")
+    path = os.path.join(root, tm.DIR_NAME[KIND])
+    eng = CrAMEngine.from_hf(AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval())
+    inputs = _dec_inputs(path)
+    calls = []
+
+    def fn(idx):
+        if die_after is not None and rank == die_after[0] and len(calls) == die_after[1]:
+            os._exit(3)                                          # killed between two decode batches
+        calls.append(list(idx))
+        return eng.generate([inputs[i][0] for i in idx], [inputs[i][1] for i in idx], DEC_HEADS, max_new_tokens=4,
+                            use_graph=False)
+
+    keys = [cdist.unit_key(ids.tolist(), w.float().tolist()) for ids, w in inputs]
+    with cpu_ops.patched_ops():
+        ans = cdist.decode_sharded(fn, NDEC, [float(x[0].numel()) for x in inputs], 2, shard_dir=shard_dir,
+                                   keys=keys, run="tiny-decode")
+    with open(f"{out_path}.calls{rank}.json", "w") as f:
+        json.dump(calls, f)
+    with open(f"{out_path}.ans{rank}.json", "w") as f:
+        json.dump(ans, f)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def dec_single(single):
+    """One process, one batch: the answers every sharded decode must reproduce."""
+    from transformers import AutoModelForCausalLM
+    from cram_amd.engine import CrAMEngine
+    from tests import cpu_ops
+    from tests import tiny_models as tm
+    root, _ = single
+    path = os.path.join(root, tm.DIR_NAME[KIND])
+    eng = CrAMEngine.from_hf(AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval())
+    inputs = _dec_inputs(path)
+    with cpu_ops.patched_ops():
+        ref = eng.generate([x[0] for x in inputs], [x[1] for x in inputs], DEC_HEADS, max_new_tokens=4,
+                           use_graph=False)
+    return root, ref
+
+
+def _dec_spawn(root, world, out, shard_dir=None, die_after=None):
+    mp.spawn(_dec_worker, args=(world, _free_port(), root, out, shard_dir, die_after), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_decode_answers_each_question_once(tmp_path, dec_single, world):
+    root, ref = dec_single
+    out = str(tmp_path / f"dec{world}")
+    _dec_spawn(root, world, out)
+    calls = [json.load(open(f"{out}.calls{r}.json")) for r in range(world)]
+    decoded = sorted(i for c in calls for b in c for i in b)
+    assert decoded == list(range(NDEC))                          # every question exactly once across ranks
+    assert all(len(b) <= 2 for c in calls for b in c)            # batches of at most `batch` rows
+    assert sum(1 for c in calls if c) == min(world, NDEC)        # every rank got work
+    for r in range(world):                                        # the full answer list on every rank
+        assert json.load(open(f"{out}.ans{r}.json")) == ref
+
+
+def test_sharded_decode_resume_after_kill(tmp_path, dec_single):
+    root, ref = dec_single
+    shards = str(tmp_path / "answers")
+    out = str(tmp_path / "dec")
+    with pytest.raises(Exception):
+        _dec_spawn(root, 2, out, shard_dir=shards, die_after=(1, 1))
+    done = cdist.read_answers(shards, "tiny-decode")
+    assert 0 < len(done) < NDEC
+    _dec_spawn(root, 2, out, shard_dir=shards)
+    calls = [json.load(open(f"{out}.calls{r}.json")) for r in range(2)]
+    redone = [i for c in calls for b in c for i in b]
+    assert len(redone) + len(done) == NDEC                       # nothing on file is decoded again
+    assert json.load(open(f"{out}.ans0.json")) == ref

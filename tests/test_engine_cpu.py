@@ -312,11 +312,13 @@ def test_sweep_flops_accounting():
     assert 0.3 * 1025 * ref_fwd < f < 0.6 * 1025 * ref_fwd
 
 
-def test_cpu_baseline_model_matches_engine():
-    """bench.py's CPU baseline runs the same network as the engine (weights copied back into transformers)."""
+@pytest.mark.parametrize("family", ["llama", "qwen2"])
+def test_cpu_baseline_model_matches_engine(family):
+    """bench.py's CPU baseline runs the same network as the engine (weights copied back into transformers; the
+    Qwen2 family with its q/k/v biases), and its decode sample runs the reference's hooked generate."""
     from cram_amd.engine import ModelSpec
     from oracle import cpu_baseline
-    sp = ModelSpec(2, 256, 4, 2, 128, 512, 1000, 1e-5, False)
+    sp = ModelSpec(2, 256, 4, 2, 128, 512, 1000, 1e-5, family == "qwen2", family)
     eng = CrAMEngine.random(sp, torch.device("cpu"), seed=3, std=0.05)
     model = cpu_baseline.hf_model_from_engine(eng)
     ids = torch.randint(0, 1000, (1, 77))
@@ -329,6 +331,21 @@ def test_cpu_baseline_model_matches_engine():
     assert (got - ref).abs().max() < 0.1 and (got - ref).abs().mean() < 0.02
     r = cpu_baseline.time_ie_units(model, ids, w, torch.tensor([5, 6]), [(0, 1), (1, 2)])
     assert r["units"] == 2 and r["units_per_s"] > 0 and all(np.isfinite(r["ie"]))
+    d = cpu_baseline.time_decode(model, ids, w, {0: [1], 1: [0, 3]}, new_tokens=100, sampled_steps=3)
+    assert d["sampled_steps"] == 3 and d["prefill_s"] > 0 and d["heads"] == 3
+    assert d["question_s"] == pytest.approx(d["prefill_s"] + 99 * d["step_s"]["median"])
+    # the hooked greedy ids of the sample equal the engine's batched decode with the same bias
+    hs = hook_ref.register_hooks(model, {0: [1], 1: [0, 3]}, hook_ref.log_weight(w))
+    try:
+        with torch.no_grad():
+            ref_ids = model.generate(input_ids=ids, attention_mask=torch.ones_like(ids), do_sample=False,
+                                     max_new_tokens=4, min_new_tokens=4, pad_token_id=0)[0, 77:].tolist()
+    finally:
+        for h in hs:
+            h.remove()
+    with cpu_ops.patched_ops():
+        got_ids = eng.generate([ids[0]], [w], {0: [1], 1: [0, 3]}, max_new_tokens=4, use_graph=False)[0]
+    assert got_ids == ref_ids
 
 
 def test_sweep_prefix_skip_is_exact(tiny, nq):

@@ -180,7 +180,12 @@ def test_full_grid_topk_sets_at_the_path_k(setup):
             fails.append(("identity", k))
         if len(O & T) < len(R & T) - slack:
             fails.append(("overlap", k, len(O & T), len(R & T), slack))
-    assert rms_o <= rms_r, (rms_o, rms_r)
+    # the bar is FROZEN as of round 3: a kernel change that fails it is a finding, not a reason to
+    # re-fit it.  The overlap slack is offset by an accuracy bar with teeth: our RMS error against the float32 truth
+    # must stay within 0.75 x the reference algorithm's own bf16 error (round 3: 0.0152 vs 0.0297 mean, 0.0208 vs
+    # 0.0408 RMS, i.e. 0.51x).
+    print(f"rms ratio ours / reference {rms_o / rms_r:.3f} (bar 0.75)")
+    assert rms_o <= 0.75 * rms_r, (rms_o, rms_r)
     assert not fails, fails
 
 

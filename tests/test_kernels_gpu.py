@@ -391,38 +391,60 @@ def test_varlen_full_size_equals_dense(gpu_device, prefill_variant):
         assert torch.equal(one[0], out[a:a + n])
 
 
-def test_decode_full_size_sampled(gpu_device):
-    """Config 2's decode step (256 sequences, 700-1100 cached keys, split-S by the engine's rule, top-half
-    heads biased with a -inf and a 0.1 span) on sampled sequences vs float64."""
+# every decode grid the bench times: (name, rows, Hq, Hkv, S_max, prompt-length range); split count by the engine's rule
+DECODE_GRIDS = [
+    ("config2_b256", 256, 32, 8, 1152, (700, 1101)),
+    ("config2_b512", 512, 32, 8, 1216, (700, 1101)),      # bench --decode-batch 512 (NQ-1000 = 2 x 500 rows)
+    ("config4_b500", 500, 28, 4, 1216, (700, 1101)),      # Qwen2-7B heads, TriviaQA-1000 = 2 x 500 rows
+    ("config5_b143", 143, 32, 8, 8448, (8000, 8349)),     # 20 docs, the KV budget's 143 rows of ~8.3k tokens
+    ("config5_b16", 16, 32, 8, 8448, (8000, 8349)),       # the round-3 config-5 batch (split-S)
+]
+
+
+@pytest.mark.parametrize("grid", DECODE_GRIDS, ids=[g[0] for g in DECODE_GRIDS])
+def test_decode_full_size_sampled(gpu_device, grid):
+    """The decode steps of the bench's grids (rows, heads, cached keys, the engine's split-S count; top-half heads
+    biased with a -inf and a 0.1 span) on sampled rows vs float64, and each sampled row bit-identical to a launch of
+    that row alone (same split count): rows never interact."""
     from cram_amd import ops
+    from cram_amd.engine import decode_attn_splits
+    _, B, Hq, Hkv, S_max, (lo, hi) = grid
     dev = gpu_device
-    B, Hq, Hkv, d, S_max = 256, 32, 8, 128, 1152
+    d, G = 128, Hq // Hkv
     g = torch.Generator(device=dev).manual_seed(5)
     q = torch.randn(B, Hq, d, generator=g, device=dev).to(torch.bfloat16)
     k = torch.randn(B, Hkv, S_max, d, generator=g, device=dev).to(torch.bfloat16)
     v = torch.randn(B, Hkv, S_max, d, generator=g, device=dev).to(torch.bfloat16)
-    lens = torch.randint(700, 1101, (B,), generator=torch.Generator().manual_seed(9))
-    W = 690
+    lens = torch.randint(lo, hi, (B,), generator=torch.Generator().manual_seed(9))
+    W = lo - 10
     w = torch.ones(B, W, dtype=torch.float16)
     w[:, 20:150] = 0.0
     w[:, 300:500] = 0.1
     bias = hook_ref.log_weight(w).to(torch.bfloat16).float()
     enable = torch.zeros(B, Hq, dtype=torch.uint8)
-    enable[:, :16] = 1
-    splits = 2
-    ws = torch.empty(ops.decode_workspace_bytes(B, Hq, d, splits), dtype=torch.uint8, device=dev)
-    out = ops.attn_decode(q, k, v, scale=d ** -0.5, seq_lens=lens.to(torch.int32).to(dev), bias=bias.to(dev),
-                          enable=enable.to(dev), W=W, num_splits=splits, workspace=ws).cpu()
+    enable[:, :Hq // 2] = 1
+    splits = decode_attn_splits(B, Hkv, S_max)
+    ws = (torch.empty(ops.decode_workspace_bytes(B, Hq, d, splits), dtype=torch.uint8, device=dev)
+          if splits > 1 else None)
+    lens_d, bias_d, en_d = lens.to(torch.int32).to(dev), bias.to(dev), enable.to(dev)
+    out = ops.attn_decode(q, k, v, scale=d ** -0.5, seq_lens=lens_d, bias=bias_d, enable=en_d, W=W,
+                          num_splits=splits, workspace=ws).cpu()
     qc, kc, vc = q.cpu(), k.cpu(), v.cpu()
-    for b in (0, 101, 255):
+    rows = sorted({0, B // 2 - 1, B - 1})
+    for b in rows:
         L = int(lens[b])
-        for h in (0, 15, 16, 31):
-            kk, vv = kc[b, h // 4, :L].double(), vc[b, h // 4, :L].double()
+        for h in sorted({0, G - 1, Hq // 2 - 1, Hq // 2, Hq - 1}):
+            kk, vv = kc[b, h // G, :L].double(), vc[b, h // G, :L].double()
             s = (kk @ qc[b, h].double()) * d ** -0.5
             if enable[b, h]:
                 s[:W] += bias[b].double()
             ref = torch.softmax(s, 0) @ vv
             _check(out[b, h][None], ref[None])
+        ws1 = (torch.empty(ops.decode_workspace_bytes(1, Hq, d, splits), dtype=torch.uint8, device=dev)
+               if splits > 1 else None)
+        one = ops.attn_decode(q[b:b + 1], k[b:b + 1], v[b:b + 1], scale=d ** -0.5, seq_lens=lens_d[b:b + 1],
+                              bias=bias_d[b:b + 1], enable=en_d[b:b + 1], W=W, num_splits=splits, workspace=ws1).cpu()
+        assert torch.equal(one[0], out[b]), f"row {b} differs from its own launch"
 
 
 def test_plain_c_host_runs(gpu_device):

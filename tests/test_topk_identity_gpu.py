@@ -119,6 +119,7 @@ def test_planted_topk_identity_at_every_separated_k(planted_model):
                "planted_ie_over_target": [float(x) for x in np.round(pos / lay.targets, 4)],
                "designed_boundaries": lay.boundaries, "asserted_k": asserted, "failed": failed,
                "gap_at_designed": {k: float(vt[k - 1] - vt[k]) for k in lay.boundaries},
+               "margin_at_designed": {k: float(vt[k - 1] - vt[k]) / bar for k in lay.boundaries},
                "random_heads_max_abs_ie": float(np.abs(np.delete(mt, [l * T.shape[2] + h for l, h in
                                                                       lay.positive() + lay.negative()])).max())}
     print("\n" + json.dumps(summary))
@@ -126,6 +127,12 @@ def test_planted_topk_identity_at_every_separated_k(planted_model):
         with open(os.environ["CRAM_TOPK_OUT"], "w") as f:
             json.dump(summary, f, indent=1)
         np.savez_compressed(os.environ["CRAM_TOPK_OUT"] + ".npz", ours=O, ref=R, truth=T)
+    margins = {k: float(vt[k - 1] - vt[k]) / bar for k in lay.boundaries}
+    print("margin (truth gap / bar) at the designed boundaries: " + json.dumps({k: round(v, 3) for k, v in margins.items()}))
     assert not failed, failed
     assert len(asserted) >= 3 and max(asserted) >= 100, asserted
     assert PATH_K in asserted, (PATH_K, asserted)
+    # every designed boundary (tier edges 10 / 50 / 100, the 130 planted h+, the path's 894) is asserted, with the
+    # truth's gap at least 1.5 x the 3 x noise bar
+    assert set(lay.boundaries) <= set(asserted), (lay.boundaries, asserted)
+    assert min(margins.values()) >= 1.5, margins

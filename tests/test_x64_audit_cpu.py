@@ -1,7 +1,7 @@
 """prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]), and so does
 prefill_x32_kernel (O = a[0:63], Q = a[64:95]); hipcc knows nothing of that ownership, so a compiler spill or copy into
 the AGPR file would silently corrupt O or Q.  cram_amd.build runs the audit
-(cram_amd.build.audit_x64) on the device assembly of every build it makes and refuses to install a library that fails
+(cram_amd.build.audit_asm_kernel) on the device assembly of every build it makes and refuses to install a library that fails
 it; this CPU test re-checks the assembly of the current build: no v_accvgpr_* instruction or AGPR operand outside the
 kernel's own inline-asm statements, no scratch traffic, and 5 wait states between any VALU write of an LDS-DMA
 descriptor SGPR and the DMA (the kernel's DMA pieces after the first of a tile carry no s_nop of their own)."""
@@ -17,21 +17,20 @@ pytestmark = pytest.mark.skipif(shutil.which("hipcc") is None and not os.path.ex
 
 
 @pytest.fixture(scope="module")
-def asm():
-    build.build()
-    if not build.x64_asm_path().exists():          # a library built before the audit existed
-        build.build(force=True)
-    return build.x64_asm_path().read_text()
+def asm(tmp_path_factory):
+    """The device assembly of the current sources: the last build's saved .s when it matches them, else a
+    device-only compile into a temporary directory (the installed library is never rebuilt or replaced here)."""
+    return build.device_asm(tmp_path_factory.mktemp("asm"))
 
 
 @pytest.mark.parametrize("kname", build.ASM_KERNELS)
 def test_asm_kernel_register_ownership_and_dma_hazards(asm, kname):
-    assert build.audit_x64(asm, kname) == []
+    assert build.audit_asm_kernel(asm, kname) == []
 
 
 @pytest.mark.parametrize("kname", build.ASM_KERNELS)
 def test_audit_catches_a_compiler_agpr_and_scratch_traffic(asm, kname):
     body = build.kernel_body(asm, kname)
-    assert build.audit_x64(asm.replace(body, body + "\n\tv_accvgpr_write_b32 a5, v1\n", 1), kname)
-    assert any("scratch" in b for b in build.audit_x64(asm.replace(body, body + "\n\tscratch_store_dword v0, v1, off\n",
+    assert build.audit_asm_kernel(asm.replace(body, body + "\n\tv_accvgpr_write_b32 a5, v1\n", 1), kname)
+    assert any("scratch" in b for b in build.audit_asm_kernel(asm.replace(body, body + "\n\tscratch_store_dword v0, v1, off\n",
                                                                                  1), kname))

@@ -1,0 +1,51 @@
+#!/bin/bash
+# The one GPU-call wrapper (replaces the round-1..3 one-off gpu_*.sh scripts).  Runs the named steps in order, each
+# under its own time limit, into gpurun_out/$TAG/; the first failing GPU step ends the call (no retries).
+#
+#   TAG=r04/x bash tools/gpu.sh STEP [STEP ...]
+#
+# steps:
+#   suite            pytest -m gpu (every GPU test, -x)
+#   suite-all        pytest -m gpu without -x (every failure listed)
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench line (config 3 + decode, CPU baselines)
+#   bench:ARGS       bench.py with ARGS (commas become spaces), e.g. bench:--config,2,--no-cpu-baseline
+#   prof             rocprofv3 --kernel-trace --stats of the sweep-only bench (summary kept, traces deleted)
+#   pmc              the attention kernel's PMC passes (tools/pmc_attn.sh) -> pmc_summary.txt + attn_pmc.json
+#   test:PATTERN     pytest -m gpu -k PATTERN
+#   py:SCRIPT,ARGS   python SCRIPT ARGS (a probe under tools/)
+set -e
+set -o pipefail
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${TAG:-run}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+PYT="python -u -m pytest tests -m gpu --timeout 300 --timeout-method thread"
+for step in "$@"; do
+  echo "== $step ($(date +%T))"
+  case "$step" in
+    suite)     timeout -k 10 1000 $PYT -x -v > $O/gputest.txt 2>&1; tail -3 $O/gputest.txt ;;
+    suite-all) timeout -k 10 1000 $PYT -v > $O/gputest.txt 2>&1 || echo "pytest rc=$?"; tail -5 $O/gputest.txt ;;
+    smoke)     timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
+               tail -2 $O/smoke.txt ;;
+    bench)     timeout -k 10 560 python -u bench.py > $O/bench.json 2> $O/bench.err; head -c 700 $O/bench.json; echo ;;
+    bench:*)   a=${step#bench:}; n=$(echo "$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+               timeout -k 10 900 python -u bench.py ${a//,/ } > $O/bench_$n.json 2> $O/bench_$n.err
+               head -c 700 $O/bench_$n.json; echo ;;
+    prof)      mkdir -p $O/prof
+               timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o sweep \
+                 -- python3 bench.py --no-cpu-baseline --no-decode > $O/prof/sweep.json 2> $O/prof/sweep.err
+               python3 tools/trace_gaps.py $O/prof > $O/prof/gaps.txt 2>&1 || true
+               find $O/prof -name "*kernel_trace.csv" -delete
+               head -8 $O/prof/sweep_kernel_stats.csv | cut -c1-160 ;;
+    pmc)       OUT=$O/pmc bash tools/pmc_attn.sh > $O/pmc_summary.txt 2>&1
+               python3 tools/pmc_to_json.py $O/pmc $O/attn_pmc.json > /dev/null; cat $O/pmc_summary.txt ;;
+    test:*)    k=${step#test:}; n=$(echo "$k" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+               timeout -k 10 900 $PYT -x -v -k "$k" > $O/test_$n.txt 2>&1; tail -3 $O/test_$n.txt ;;
+    py:*)      a=${step#py:}; n=$(basename "${a%%,*}" .py)
+               timeout -k 10 600 python -u ${a//,/ } > $O/$n.txt 2>&1; tail -30 $O/$n.txt ;;
+    *)         echo "unknown step $step"; exit 2 ;;
+  esac
+done

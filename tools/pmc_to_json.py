@@ -1,47 +1,103 @@
-"""profiles/<dir>/p{3,4}_counter_collection.csv -> profiles/attn_pmc.json (HBM bytes per prefill launch).
+"""rocprofv3 PMC passes of the IE-sweep attention launch -> profiles/attn_pmc.json.
 
-Corrections per MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
-FETCH_SIZE counts half the bytes of 16 B/lane streaming reads (double it), WRITE_SIZE is exact for
-16 B/lane stores.  The PMC shape is tools/prof_attn.py's default (the IE-sweep attention launch).
+Input: the directory tools/pmc_attn.sh wrote (p1..p5/p*_counter_collection.csv, one --pmc pass each, kernel-trace
+only), or a directory holding them further down.  Output: what the north star asks rocprof to report for the
+attention kernel — achieved HBM GB/s and MFMA utilisation against the gfx950 peak — plus the issue statistics,
+tied to the kernel source hash of the build the passes ran on (bench.py copies them into its `roofline` only
+when the running build hashes the same).
+
+Corrections and units (MI355X_MICROARCH.md, HBM / rocprofv3 and the PMC-units row):
+  * FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE counts half the bytes of 16 B/lane streaming reads
+    (doubled here); WRITE_SIZE is exact for 16 B/lane stores;
+  * GRBM_GUI_ACTIVE is summed over the 8 XCDs: kernel clock cycles = GRBM_GUI_ACTIVE / 8, effective clock =
+    that / the dispatch's wall time (its Start/End timestamps in the same CSV);
+  * SQ_VALU_MFMA_BUSY_CYCLES counts matrix-pipe cycles summed over the SIMDs (32 per v_mfma_f32_32x32x16_bf16), so
+    mfma_busy = MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) = the fraction of SIMD-cycles the matrix pipe works;
+  * MFMA issues x 32768 FLOP against the launch's algorithmic FLOPs counts the masked work that is still issued
+    (half-masked diagonal blocks, the 32-key rounding of each block's last key).
 """
+import collections
 import csv
+import glob
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
 from cram_amd.build import kernel_source_hash  # noqa: E402
 from cram_amd.ops import prefill_work  # noqa: E402
 
-src = sys.argv[1] if len(sys.argv) > 1 else "profiles/r01_pmc"
-B, T, Hq, Hkv, d = 33, 962, 32, 8, 128
+B, T, Hq, Hkv, d = 33, 962, 32, 8, 128          # tools/prof_attn.py's default: the IE sweep's attention launch
+SIMDS = 1024                                     # 256 CUs x 4 SIMDs
+XCDS = 8
+MFMA_FLOP = 32 * 32 * 16 * 2                     # v_mfma_f32_32x32x16_bf16
+PEAK_TFLOPS, PEAK_GBS = 2500.0, 8000.0           # dense bf16 MFMA, HBM3E (MI355X_MICROARCH.md chip table)
 
 
-KERNELS = set()
+def load(src):
+    """{counter: [(value, duration_ns), ...]} over every dispatch of the attention kernel in every pass."""
+    files = sorted(glob.glob(os.path.join(src, "**", "p*_counter_collection.csv"), recursive=True))
+    if not files:
+        raise SystemExit(f"no p*_counter_collection.csv under {src}")
+    out = collections.defaultdict(list)
+    kernels = set()
+    for fn in files:
+        for r in csv.DictReader(open(fn)):
+            kernels.add(r.get("Kernel_Name", "?"))
+            dur = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+            out[r["Counter_Name"]].append((float(r["Counter_Value"]), dur))
+    return out, kernels
 
 
-def mean(name, f):
-    import glob
-    hits = [os.path.join(src, f)] if os.path.exists(os.path.join(src, f)) else \
-        sorted(glob.glob(os.path.join(src, "**", f), recursive=True))
-    rows = [r for r in csv.DictReader(open(hits[0])) if r["Counter_Name"] == name]
-    KERNELS.update(r.get("Kernel_Name", "?") for r in rows)
-    v = [float(r["Counter_Value"]) for r in rows]
-    return sum(v) / len(v), len(v)
+def mean(rows, what=0):
+    return sum(x[what] for x in rows) / len(rows)
 
 
-fetch_kib, n = mean("FETCH_SIZE", "p3_counter_collection.csv")
-write_kib, _ = mean("WRITE_SIZE", "p4_counter_collection.csv")
-read_b = fetch_kib * 1024 * 2
-write_b = write_kib * 1024
-_, alg = prefill_work(B, Hq, Hkv, T, T, d, 0)
-out = {"kernel": " / ".join(sorted(KERNELS)), "shape": {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d}, "dispatches": n,
-       "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "hbm_read_bytes": read_b, "hbm_write_bytes": write_b,
-       "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": alg,
-       "traffic_over_algorithmic": (read_b + write_b) / alg,
-       "source": os.path.relpath(os.path.abspath(src), os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-       "kernel_source_hash": kernel_source_hash(),
-       "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc_attn.sh); FETCH_SIZE x2 "
-               "(gfx950 16B/lane read undercount), KiB -> B"}
-json.dump(out, open("profiles/attn_pmc.json", "w"), indent=1)
-print(json.dumps(out, indent=1))
+def main():
+    src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "attn_pmc.json")
+    c, kernels = load(src)
+    flops, alg_bytes = prefill_work(B, Hq, Hkv, T, T, d, 0)
+    read_b = mean(c["FETCH_SIZE"]) * 1024 * 2
+    write_b = mean(c["WRITE_SIZE"]) * 1024
+    traffic = read_b + write_b
+    # wall time per dispatch under the traffic passes (counters of those passes do not slow the kernel measurably)
+    t_traffic = (mean(c["FETCH_SIZE"], 1) + mean(c["WRITE_SIZE"], 1)) / 2 * 1e-9
+    grbm = mean(c["GRBM_GUI_ACTIVE"])
+    t_grbm = mean(c["GRBM_GUI_ACTIVE"], 1) * 1e-9
+    cycles = grbm / XCDS
+    clock_ghz = cycles / t_grbm / 1e9
+    mfma_busy = mean(c["SQ_VALU_MFMA_BUSY_CYCLES"]) / (cycles * SIMDS)
+    n_mfma = mean(c["SQ_INSTS_MFMA"])
+    out = {
+        "kernel": " / ".join(sorted(kernels)),
+        "shape": {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d},
+        "dispatches": len(c["FETCH_SIZE"]),
+        "fetch_size_kib": mean(c["FETCH_SIZE"]), "write_size_kib": mean(c["WRITE_SIZE"]),
+        "hbm_read_bytes": read_b, "hbm_write_bytes": write_b, "hbm_bytes_per_launch": traffic,
+        "algorithmic_bytes_per_launch": alg_bytes, "traffic_over_algorithmic": traffic / alg_bytes,
+        "avg_launch_ms_under_pmc": round(t_traffic * 1e3, 4),
+        "hbm_gbs": round(traffic / t_traffic / 1e9, 1),
+        "hbm_frac": round(traffic / t_traffic / 1e9 / PEAK_GBS, 4),
+        "tflops": round(flops / t_traffic / 1e12, 1),
+        "mfma_frac_of_peak": round(flops / t_traffic / 1e12 / PEAK_TFLOPS, 4),
+        "mfma_busy": round(mfma_busy, 4),
+        "effective_clock_ghz": round(clock_ghz, 3),
+        "valu_per_mfma": round(mean(c["SQ_INSTS_VALU"]) / n_mfma, 2),
+        "mfma_issues_over_algorithmic": round(n_mfma * MFMA_FLOP / flops, 4),
+        "wait_any_frac": round(mean(c["SQ_WAIT_ANY"]) / mean(c["SQ_WAVE_CYCLES"]), 4),
+        "lds_bank_conflict_per_lds_inst": round(mean(c["SQ_LDS_BANK_CONFLICT"]) / mean(c["SQ_INSTS_LDS"]), 4),
+        "source": os.path.relpath(os.path.abspath(src), REPO),
+        "kernel_source_hash": kernel_source_hash(),
+        "note": ("rocprofv3 --pmc in separate passes (tools/pmc_attn.sh). traffic: FETCH_SIZE x2 (gfx950 16 B/lane "
+                 "read undercount) + WRITE_SIZE, KiB -> B; hbm_gbs / tflops: over the dispatches' own wall time; "
+                 "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); effective clock = "
+                 "GRBM_GUI_ACTIVE / 8 / wall; mfma issues x 32768 FLOP / algorithmic FLOPs"),
+    }
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
