@@ -110,6 +110,7 @@ def check(code: int, what: str) -> None:
 KNOB_PREFILL_VARIANT = 0   # CRAM_KNOB_PREFILL_VARIANT
 KNOB_DECODE_U = 1          # CRAM_KNOB_DECODE_U
 KNOB_DECODE_MFMA = 2       # CRAM_KNOB_DECODE_MFMA
+KNOB_GEMM_VARIANT = 3      # CRAM_KNOB_GEMM_VARIANT
 
 
 def set_knob(which: int, value: int) -> int:

@@ -18,7 +18,8 @@ REPO_DIR = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc"
 LIB_PATH = PKG_DIR / "libcram_attn.so"
 SOURCES = [CSRC / "cram_attn.hip", CSRC / "cram_fused.hip", CSRC / "cram_gemm.hip", CSRC / "cram_spans.cpp"]
-HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc"]
+HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc",
+           CSRC / "gemm_w4_loop.inc"]
 ARCH = "gfx950"
 
 

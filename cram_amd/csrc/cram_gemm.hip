@@ -88,7 +88,8 @@ struct GemmParams {
   void* out; int64_t ldo;          // [M, N] (store) or [M, N / 2] (silu-mul); EPI_PARTIAL: fp32 [splits][M][N]
   int M, N, K;
   int ntm, ntn, nblocks;
-  int splits, kts;                 // split-K: K ranges per output tile, K-tiles per range (K = splits * kts * BK)
+  int splits, kts;
+  int raster;                      // gemm_w4_kernel tile order (tile_of_w4); 0 = the default                 // split-K: K ranges per output tile, K-tiles per range (K = splits * kts * BK)
 };
 
 __device__ __forceinline__ void barrier() {
@@ -315,6 +316,192 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
   store_tile<T, EPI, 8, 4>(acc, pp, m0 + yrow0 + fr, n0 + xrow0 + 4 * fg);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// gemm_w4_kernel: 4 waves (one per SIMD), 128 x 128 outputs per wave in a[0:255], the hand-placed stream of
+// tools/gen_gemm_w4.py (gemm_w4_loop.inc): every fragment read, LDS-DMA piece, barrier and counter wait sits in a gap
+// between two MFMAs, three barriers per 64-deep K-tile, prefetch one tile ahead through a two-stage LDS ring.  The
+// shape of the vendor's 256 x 256 x 64 kernel (the one hipBLASLt picks for the sweep's projections), with this
+// library's epilogues.  bf16 / fp16, K-tiles per range >= 2.
+// ---------------------------------------------------------------------------------------------------------------
+#include "gemm_w4_loop.inc"
+
+constexpr int W4_LDS = 2 * 65536;              // two stages of (weight image 32 KiB | activation image 32 KiB)
+
+#define CRAM_V128_255_CLOBBERS                                                                                       \
+  "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141",    \
+  "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155",    \
+  "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169",    \
+  "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183",    \
+  "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197",    \
+  "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211",    \
+  "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225",    \
+  "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239",    \
+  "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253",    \
+  "v254", "v255"
+#define CRAM_A_CLOBBERS_10(b)                                                                                        \
+  "a" #b "0", "a" #b "1", "a" #b "2", "a" #b "3", "a" #b "4", "a" #b "5", "a" #b "6", "a" #b "7", "a" #b "8",       \
+  "a" #b "9"
+// a0..a255 spelled out (the clobbers size the kernel's accumulator file)
+#define CRAM_A256_CLOBBERS                                                                                           \
+  "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", CRAM_A_CLOBBERS_10(1), CRAM_A_CLOBBERS_10(2),          \
+  CRAM_A_CLOBBERS_10(3), CRAM_A_CLOBBERS_10(4), CRAM_A_CLOBBERS_10(5), CRAM_A_CLOBBERS_10(6), CRAM_A_CLOBBERS_10(7),  \
+  CRAM_A_CLOBBERS_10(8), CRAM_A_CLOBBERS_10(9), CRAM_A_CLOBBERS_10(10), CRAM_A_CLOBBERS_10(11),                      \
+  CRAM_A_CLOBBERS_10(12), CRAM_A_CLOBBERS_10(13), CRAM_A_CLOBBERS_10(14), CRAM_A_CLOBBERS_10(15),                    \
+  CRAM_A_CLOBBERS_10(16), CRAM_A_CLOBBERS_10(17), CRAM_A_CLOBBERS_10(18), CRAM_A_CLOBBERS_10(19),                    \
+  CRAM_A_CLOBBERS_10(20), CRAM_A_CLOBBERS_10(21), CRAM_A_CLOBBERS_10(22), CRAM_A_CLOBBERS_10(23),                    \
+  CRAM_A_CLOBBERS_10(24), "a250", "a251", "a252", "a253", "a254", "a255"
+
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
+template <int A>
+__device__ __forceinline__ f32x4 acc4() {      // accumulator tile a[A .. A + 3]
+  f32x4 v;
+  asm volatile("v_accvgpr_read_b32 %0, a[%c4]\n\tv_accvgpr_read_b32 %1, a[%c4+1]\n\t"
+               "v_accvgpr_read_b32 %2, a[%c4+2]\n\tv_accvgpr_read_b32 %3, a[%c4+3]"
+               : "=v"(v[0]), "=v"(v[1]), "=v"(v[2]), "=v"(v[3]) : "i"(A));
+  return v;
+}
+
+__device__ __forceinline__ u32x4 w4_srd(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  u32x4 d;
+  d[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  d[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+  d[2] = __builtin_amdgcn_readfirstlane(bytes);
+  d[3] = 0x00020000u;
+  return d;
+}
+
+// tile order of the 4-wave kernel: the XCD-bijective remap of tile_of, then groups of GN weight tiles (activation
+// tiles innermost) or GM activation tiles (weight tiles innermost)
+__device__ __forceinline__ void tile_of_w4(const GemmParams& p, int bid, int& tm, int& tn) {
+  int wid = bid;
+  if (p.raster != 3) {
+    const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
+    wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  }
+  if (p.raster == 2) {
+    constexpr int GM = 8;
+    const int grp = wid / (GM * p.ntn);
+    const int gw = min(GM, p.ntm - grp * GM);
+    const int rem = wid - grp * GM * p.ntn;
+    tm = grp * GM + rem % gw;
+    tn = rem / gw;
+    return;
+  }
+  const int GN = p.raster == 1 ? 16 : 8;
+  const int grp = wid / (GN * p.ntm);
+  const int gw = min(GN, p.ntn - grp * GN);
+  const int rem = wid - grp * GN * p.ntm;
+  tn = grp * GN + rem % gw;
+  tm = rem / gw;
+}
+
+template <typename T, int EPI, int LV>
+__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(1024))) char smem[W4_LDS];
+  int tm, tn;
+  tile_of_w4(p, blockIdx.x, tm, tn);
+  const int n0 = tn * BN, m0 = tm * BM;
+  const int kc = p.kts * BK;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 1, wm = wave >> 1;
+
+  const T* xb = static_cast<const T*>(p.x) + (int64_t)n0 * p.ldx;
+  const T* yb = static_cast<const T*>(p.y) + (int64_t)m0 * p.ldy;
+  const int yrows = min(BM, p.M - m0);
+  // rows live in the per-lane voffset (range-checked: a row at or past M reads zeros), the K-tile in soffset
+  u32x4 sx = w4_srd(xb, (uint32_t)((BN - 1) * p.ldx * 2 + kc * 2));
+  u32x4 sy = w4_srd(yb, (uint32_t)((yrows - 1) * p.ldy * 2 + kc * 2));
+  // LDS-DMA piece i of this wave: image rows 64 wave + 8 i .. +7; lane L fetches row + L / 8, chunk (L % 8) ^ swz(row)
+  uint32_t vx[8], vy[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = 64 * wave + 8 * i + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    vx[i] = (uint32_t)(row * p.ldx * 2 + c * 16);
+    vy[i] = (uint32_t)(row * p.ldy * 2 + c * 16);
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
+  uint32_t mx = __builtin_amdgcn_readfirstlane(lds0 + 8192 * wave);
+  uint32_t my = __builtin_amdgcn_readfirstlane(lds0 + 32768 + 8192 * wave);
+  uint32_t so = 0;
+  // fragment reads: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row fragment, k chunk 4 ks + g
+  const int fr = lane & 15, fg = lane >> 4;
+  uint32_t rx0 = lds0 + (128 * wn + fr) * ROWB + ((fg ^ (fr >> 1)) * 16);
+  uint32_t rx1 = lds0 + (128 * wn + fr) * ROWB + (((4 + fg) ^ (fr >> 1)) * 16);
+  uint32_t ry0 = lds0 + 32768 + (128 * wm + fr) * ROWB + ((fg ^ (fr >> 1)) * 16);
+  uint32_t ry1 = lds0 + 32768 + (128 * wm + fr) * ROWB + (((4 + fg) ^ (fr >> 1)) * 16);
+  uint32_t n = (uint32_t)(p.kts - 2);
+  uint32_t keep;
+#define CRAM_W4_ASM(LOOP, TY)                                                                                        \
+  asm volatile("s_mov_b32 %[keep], m0\n\t"                                                                           \
+               "v_accvgpr_write_b32 a0, 0\n\t.set cram_w4i, 1\n\t.rept 255\n\t"                                      \
+               "v_accvgpr_write_b32 a[cram_w4i], 0\n\t.set cram_w4i, cram_w4i+1\n\t.endr\n\t"                         \
+               LOOP(TY)                                                                                              \
+               "s_mov_b32 m0, %[keep]"                                                                               \
+               : [keep] "=&s"(keep), [rx0] "+v"(rx0), [rx1] "+v"(rx1), [ry0] "+v"(ry0), [ry1] "+v"(ry1),               \
+                 [mx] "+s"(mx), [my] "+s"(my), [so] "+s"(so), [n] "+s"(n)                                            \
+               : [sx] "s"(sx), [sy] "s"(sy), [vx0] "v"(vx[0]), [vx1] "v"(vx[1]), [vx2] "v"(vx[2]), [vx3] "v"(vx[3]), \
+                 [vx4] "v"(vx[4]), [vx5] "v"(vx[5]), [vx6] "v"(vx[6]), [vx7] "v"(vx[7]), [vy0] "v"(vy[0]),           \
+                 [vy1] "v"(vy[1]), [vy2] "v"(vy[2]), [vy3] "v"(vy[3]), [vy4] "v"(vy[4]), [vy5] "v"(vy[5]),           \
+                 [vy6] "v"(vy[6]), [vy7] "v"(vy[7])                                                                  \
+               : "memory", "scc", CRAM_V128_255_CLOBBERS, CRAM_A256_CLOBBERS)
+  if constexpr (LV == 0) {
+    if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "bf16");
+    else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "f16");
+  } else {
+    if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_B, "bf16");
+    else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_B, "f16");
+  }
+#undef CRAM_W4_ASM
+
+  // epilogue: lane (r, g) holds acc tile (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]
+  const int mrow = m0 + 128 * wm + fr;
+  const int ncol = n0 + 128 * wn + 4 * fg;
+  using V4 = typename GVec<T>::x4;
+  T* ob = static_cast<T*>(p.out);
+  static_for<8>([&](auto bi) {
+    constexpr int b = decltype(bi)::value;
+    const int m = mrow + 16 * b;
+    if (m < p.M) {
+      if constexpr (EPI == CRAM_GEMM_STORE) {
+        static_for<8>([&](auto ai) {
+          constexpr int a = decltype(ai)::value;
+          const f32x4 v = acc4<4 * (8 * a + b)>();
+          V4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = (T)v[i];
+          *reinterpret_cast<V4*>(ob + (int64_t)m * p.ldo + ncol + 16 * a) = o;
+        });
+      } else {
+        // gate tiles a = 0, 1, 4, 5 and their up tiles a + 2 (weight rows interleaved in blocks of 32): gate column
+        // n' = n + 16 a is output column f = 32 (n' / 64) + n' % 64
+        static_for<4>([&](auto ji) {
+          constexpr int a = (decltype(ji)::value & 1) + 4 * (decltype(ji)::value >> 1);
+          const f32x4 gv = acc4<4 * (8 * a + b)>(), uv = acc4<4 * (8 * (a + 2) + b)>();
+          const int ng = ncol + 16 * a;
+          const int f = 32 * (ng >> 6) + (ng & 63);
+          V4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float g = rnd<T>(gv[i]), u = rnd<T>(uv[i]);
+            o[i] = (T)(rnd<T>(g / (1.0f + expf(-g))) * u);
+          }
+          *reinterpret_cast<V4*>(ob + (int64_t)m * p.ldo + f) = o;
+        });
+      }
+    }
+  });
+}
+
 // Split-K combine: out = epilogue(sum over the K ranges of the fp32 partials [splits][M][N], in range order — the
 // result does not depend on which workgroup finished first).  One thread per 8 output columns of one row.
 //   CRAM_GEMM_STORE         out[m, n] = rnd(sum + bias[n])            (bias optional: F.linear's addmm epilogue)
@@ -391,6 +578,21 @@ extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx,
   p.nblocks = (int)nb;
   const hipStream_t st = (hipStream_t)stream;
   const dim3 g(p.nblocks);
+  int kv = -1;
+  cram_get_knob(CRAM_KNOB_GEMM_VARIANT, &kv);
+  // A/B of the 4-wave kernel (knob 1..4): loop variant A / B x tile order (weight-tile groups / activation-tile groups)
+  p.raster = (kv == 3 || kv == 4) ? 2 : 0;
+  const bool lb = kv == 2 || kv == 4;
+  if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && kv != 0) {
+    if (epilogue == CRAM_GEMM_STORE) {
+      if (lb) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE, 1>), g, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE, 0>), g, dim3(256), 0, st, p);
+    } else {
+      if (lb) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL, 1>), g, dim3(256), 0, st, p);
+      else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL, 0>), g, dim3(256), 0, st, p);
+    }
+    return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+  }
   const dim3 blk(512);
   if (dtype == CRAM_DTYPE_BF16) {
     if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<__bf16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
@@ -425,7 +627,7 @@ extern "C" int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64
   GemmParams p;
   p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = workspace; p.ldo = N;
   p.M = M; p.N = N; p.K = K;
-  p.splits = splits; p.kts = K / (BK * splits);
+  p.splits = splits; p.kts = K / (BK * splits); p.raster = 0;
   p.ntm = (M + BM - 1) / BM;
   p.ntn = N / BN;
   const int64_t nb = (int64_t)p.ntm * p.ntn * splits;

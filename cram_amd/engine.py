@@ -80,6 +80,8 @@ class ModelSpec:
 
 
 ROW_ALIGN = 256
+# gate/up + SiLU-mul on cram_gemm's fused epilogue (CrAMEngine.mlp); CRAM_FUSED_MLP=0: hipBLASLt + cram_silu_mul (A/B)
+FUSED_MLP = os.environ.get("CRAM_FUSED_MLP", "1") != "0"
 # packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where hipBLASLt already runs at full rate
 PREFILL_CHUNK_ROWS = 32768
 
@@ -131,7 +133,7 @@ def configure_blas(lib: str = "hipblas") -> None:
 
 
 class LayerW:
-    __slots__ = ("ln1", "wqkv", "bqkv", "wo", "ln2", "wgu", "wd")
+    __slots__ = ("ln1", "wqkv", "bqkv", "wo", "ln2", "wgu", "wd", "wgu_il", "wgu_il_key")
 
 
 class CrAMEngine:
@@ -226,8 +228,35 @@ class CrAMEngine:
         return (emb.cos() * self.attn_scaling).to(self.dtype), (emb.sin() * self.attn_scaling).to(self.dtype)
 
     def mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
-        gu = ops.linear(x, lw.wgu)
-        return ops.linear(ops.silu_mul(gu, self.spec.intermediate), lw.wd)
+        """LlamaMLP: down(rnd(silu(gate)) * up).  Row counts of the sweep and the packed prefill run gate/up on
+        cram_gemm's 4-wave kernel with the SiLU-mul in its epilogue (the [M, 2F] projection never reaches HBM;
+        1.05x hipBLASLt + cram_silu_mul at M = 29k, tools/gemm_ab_knob.py), same rounding points as the pair."""
+        F = self.spec.intermediate
+        if self._fused_mlp_ok(x):
+            act = ops.gemm(x, self._gate_up_interleaved(lw), ops.GEMM_SILU_MUL)
+        else:
+            act = ops.silu_mul(ops.linear(x, lw.wgu), F)
+        return ops.linear(act, lw.wd)
+
+    # gate/up with the fused activation: bf16 (the 4-wave kernel's type), 256-row tiles filled, the weight interleaved
+    FUSED_MLP_MIN_ROWS = 4096
+
+    def _fused_mlp_ok(self, x: torch.Tensor) -> bool:
+        if not FUSED_MLP or self.device.type != "cuda" or self.dtype != torch.bfloat16:
+            return False
+        D, F = self.spec.hidden, self.spec.intermediate
+        M = x.numel() // x.shape[-1]
+        return M >= self.FUSED_MLP_MIN_ROWS and (2 * F) % 256 == 0 and D % 64 == 0 and D >= 128
+
+    def _gate_up_interleaved(self, lw: LayerW) -> torch.Tensor:
+        """lw.wgu with gate / up rows interleaved in blocks of 32 (cram_gemm's SiLU-mul layout), rebuilt whenever the
+        checkpoint weight changes (tensor identity + torch's in-place version counter)."""
+        w = lw.wgu
+        key = (w.data_ptr(), w._version)
+        if getattr(lw, "wgu_il_key", None) != key:
+            lw.wgu_il = ops.interleave_gate_up(w, self.spec.intermediate).contiguous()
+            lw.wgu_il_key = key
+        return lw.wgu_il
 
     def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin, pos: Optional[torch.Tensor] = None):
         """x [B, T, D] -> roped q [B, T, Hq, d], k / v [B, T, Hkv, d]: strided views of one fused buffer."""

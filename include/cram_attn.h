@@ -61,7 +61,8 @@ int cram_abi_version(void);
 
 /*
  * Process-wide kernel-selection knobs (A/B runs and tests; the product default is automatic = -1).
- * The initial values are read once from the environment (CRAM_PREFILL_VARIANT, CRAM_DECODE_U, CRAM_DECODE_MFMA) at
+ * The initial values are read once from the environment (CRAM_PREFILL_VARIANT, CRAM_DECODE_U, CRAM_DECODE_MFMA,
+ * CRAM_GEMM_VARIANT) at
  * the first query (once per process, thread-safe); no launch reads the environment.  Knob values are atomics:
  * a value set from one thread is seen by launches issued afterwards from any thread.
  *   CRAM_KNOB_PREFILL_VARIANT  -1 = automatic: 64-key tiles, 4 waves, except GQA-7 groups with sequences <= 2048
@@ -72,6 +73,9 @@ int cram_abi_version(void);
  *                              per wave, hand-ordered stream (bf16, d = 128, GQA groups of 4k; otherwise as 0)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
+ *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles on the 4-wave 128 x 128-per-wave
+ *                              kernel (1), others on the 8-wave kernel (0); 0 / 1 force one (1 falls back to 0 where
+ *                              it does not apply)
  * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob stores the value in
  * *value and returns CRAM_OK, or CRAM_ERR_INVALID_ARG for an unknown knob / null pointer (ABI 4: the value -1,
  * "automatic", is never an error code).
@@ -79,7 +83,8 @@ int cram_abi_version(void);
 #define CRAM_KNOB_PREFILL_VARIANT 0
 #define CRAM_KNOB_DECODE_U 1
 #define CRAM_KNOB_DECODE_MFMA 2
-#define CRAM_KNOB_COUNT 3
+#define CRAM_KNOB_GEMM_VARIANT 3
+#define CRAM_KNOB_COUNT 4
 int cram_set_knob(int which, int value);
 int cram_get_knob(int which, int* value);
 
