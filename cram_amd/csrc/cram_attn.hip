@@ -1046,7 +1046,7 @@ inline void knobs_init() {
     const char* em = getenv("CRAM_DECODE_MFMA");
     g_knob[CRAM_KNOB_DECODE_MFMA].store((em && (em[0] == '0' || em[0] == '1')) ? em[0] - '0' : -1);
     const char* eg = getenv("CRAM_GEMM_VARIANT");
-    g_knob[CRAM_KNOB_GEMM_VARIANT].store((eg && eg[0] >= '0' && eg[0] <= '4') ? eg[0] - '0' : -1);
+    g_knob[CRAM_KNOB_GEMM_VARIANT].store((eg && eg[0] >= '0' && eg[0] <= '2') ? eg[0] - '0' : -1);
   });
 }
 inline int knob(int k) {
@@ -1206,7 +1206,7 @@ int cram_set_knob(int which, int value) {
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_MFMA && value != -1 && value != 0 && value != 1) return CRAM_ERR_INVALID_ARG;
-  if (which == CRAM_KNOB_GEMM_VARIANT && (value < -1 || value > 4)) return CRAM_ERR_INVALID_ARG;
+  if (which == CRAM_KNOB_GEMM_VARIANT && (value < -1 || value > 2)) return CRAM_ERR_INVALID_ARG;
   g_knob[which].store(value);
   return CRAM_OK;
 }

@@ -88,8 +88,8 @@ struct GemmParams {
   void* out; int64_t ldo;          // [M, N] (store) or [M, N / 2] (silu-mul); EPI_PARTIAL: fp32 [splits][M][N]
   int M, N, K;
   int ntm, ntn, nblocks;
-  int splits, kts;
-  int raster;                      // gemm_w4_kernel tile order (tile_of_w4); 0 = the default                 // split-K: K ranges per output tile, K-tiles per range (K = splits * kts * BK)
+  int splits, kts;                 // split-K: K ranges per output tile, K-tiles per range (K = splits * kts * BK)
+  int raster;                      // gemm_w4_kernel tile order (tile_of_w4); 0 = the default
 };
 
 __device__ __forceinline__ void barrier() {
@@ -378,32 +378,29 @@ __device__ __forceinline__ u32x4 w4_srd(const void* base, uint32_t bytes) {
   return d;
 }
 
-// tile order of the 4-wave kernel: the XCD-bijective remap of tile_of, then groups of GN weight tiles (activation
-// tiles innermost) or GM activation tiles (weight tiles innermost)
+// tile order of the 4-wave kernel: the XCD-bijective remap of tile_of, then groups of 8 weight tiles (activation
+// tiles innermost) or of 8 activation tiles (weight tiles innermost); measured alternatives (r04, tools/gemm_ab_knob.py):
+// groups of 16 weight tiles 0.92-0.95x, no XCD remap 0.86-0.95x
 __device__ __forceinline__ void tile_of_w4(const GemmParams& p, int bid, int& tm, int& tn) {
-  int wid = bid;
-  if (p.raster != 3) {
-    const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
-    wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  }
-  if (p.raster == 2) {
-    constexpr int GM = 8;
-    const int grp = wid / (GM * p.ntn);
-    const int gw = min(GM, p.ntm - grp * GM);
-    const int rem = wid - grp * GM * p.ntn;
-    tm = grp * GM + rem % gw;
+  const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
+  const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  constexpr int G = 8;
+  if (p.raster == 2) {                           // groups of 8 activation tiles, weight tiles innermost
+    const int grp = wid / (G * p.ntn);
+    const int gw = min(G, p.ntm - grp * G);
+    const int rem = wid - grp * G * p.ntn;
+    tm = grp * G + rem % gw;
     tn = rem / gw;
-    return;
+  } else {                                       // groups of 8 weight tiles, activation tiles innermost
+    const int grp = wid / (G * p.ntm);
+    const int gw = min(G, p.ntn - grp * G);
+    const int rem = wid - grp * G * p.ntm;
+    tn = grp * G + rem % gw;
+    tm = rem / gw;
   }
-  const int GN = p.raster == 1 ? 16 : 8;
-  const int grp = wid / (GN * p.ntm);
-  const int gw = min(GN, p.ntn - grp * GN);
-  const int rem = wid - grp * GN * p.ntm;
-  tn = grp * GN + rem % gw;
-  tm = rem / gw;
 }
 
-template <typename T, int EPI, int LV>
+template <typename T, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[W4_LDS];
   int tm, tn;
@@ -432,7 +429,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
   uint32_t mx = __builtin_amdgcn_readfirstlane(lds0 + 8192 * wave);
   uint32_t my = __builtin_amdgcn_readfirstlane(lds0 + 32768 + 8192 * wave);
+  // K offset of the next tile to stage (soffset); kend wraps it (the generated loop supports a rotated K start: a
+  // staggered start per workgroup measured 0.97-0.99x, r04, so every workgroup starts at tile 0)
   uint32_t so = 0;
+  const uint32_t kend = (uint32_t)(p.kts * ROWB);
   // fragment reads: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row fragment, k chunk 4 ks + g
   const int fr = lane & 15, fg = lane >> 4;
   uint32_t rx0 = lds0 + (128 * wn + fr) * ROWB + ((fg ^ (fr >> 1)) * 16);
@@ -449,18 +449,13 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
                "s_mov_b32 m0, %[keep]"                                                                               \
                : [keep] "=&s"(keep), [rx0] "+v"(rx0), [rx1] "+v"(rx1), [ry0] "+v"(ry0), [ry1] "+v"(ry1),               \
                  [mx] "+s"(mx), [my] "+s"(my), [so] "+s"(so), [n] "+s"(n)                                            \
-               : [sx] "s"(sx), [sy] "s"(sy), [vx0] "v"(vx[0]), [vx1] "v"(vx[1]), [vx2] "v"(vx[2]), [vx3] "v"(vx[3]), \
+               : [sx] "s"(sx), [sy] "s"(sy), [kend] "s"(kend), [vx0] "v"(vx[0]), [vx1] "v"(vx[1]), [vx2] "v"(vx[2]), [vx3] "v"(vx[3]), \
                  [vx4] "v"(vx[4]), [vx5] "v"(vx[5]), [vx6] "v"(vx[6]), [vx7] "v"(vx[7]), [vy0] "v"(vy[0]),           \
                  [vy1] "v"(vy[1]), [vy2] "v"(vy[2]), [vy3] "v"(vy[3]), [vy4] "v"(vy[4]), [vy5] "v"(vy[5]),           \
                  [vy6] "v"(vy[6]), [vy7] "v"(vy[7])                                                                  \
                : "memory", "scc", CRAM_V128_255_CLOBBERS, CRAM_A256_CLOBBERS)
-  if constexpr (LV == 0) {
-    if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "bf16");
-    else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "f16");
-  } else {
-    if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_B, "bf16");
-    else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_B, "f16");
-  }
+  if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "bf16");
+  else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "f16");
 #undef CRAM_W4_ASM
 
   // epilogue: lane (r, g) holds acc tile (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]
@@ -580,17 +575,12 @@ extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx,
   const dim3 g(p.nblocks);
   int kv = -1;
   cram_get_knob(CRAM_KNOB_GEMM_VARIANT, &kv);
-  // A/B of the 4-wave kernel (knob 1..4): loop variant A / B x tile order (weight-tile groups / activation-tile groups)
-  p.raster = (kv == 3 || kv == 4) ? 2 : 0;
-  const bool lb = kv == 2 || kv == 4;
+  // knob 1 / -1: the 4-wave kernel, tile order by weight-tile groups (best for gate/up and down); 2: activation-tile
+  // groups (A/B; 1.00-1.03x on q/k/v and o_proj, 0.94x on down, r04)
+  p.raster = kv == 2 ? 2 : 0;
   if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && kv != 0) {
-    if (epilogue == CRAM_GEMM_STORE) {
-      if (lb) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE, 1>), g, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE, 0>), g, dim3(256), 0, st, p);
-    } else {
-      if (lb) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL, 1>), g, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL, 0>), g, dim3(256), 0, st, p);
-    }
+    if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE>), g, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL>), g, dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
   }
   const dim3 blk(512);

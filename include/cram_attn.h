@@ -75,7 +75,7 @@ int cram_abi_version(void);
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
  *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles on the 4-wave 128 x 128-per-wave
  *                              kernel (1), others on the 8-wave kernel (0); 0 / 1 force one (1 falls back to 0 where
- *                              it does not apply)
+ *                              it does not apply); 2 = the 4-wave kernel with its alternative tile order (A/B)
  * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob stores the value in
  * *value and returns CRAM_OK, or CRAM_ERR_INVALID_ARG for an unknown knob / null pointer (ABI 4: the value -1,
  * "automatic", is never an error code).

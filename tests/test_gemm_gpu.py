@@ -15,6 +15,16 @@ from cram_amd import ops
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["auto", "8wave", "w4", "w4_alt_order"])
+def gemm_variant(request):
+    """Run a cram_gemm test on each kernel: the automatic choice (bf16 with >= 2 K-tiles -> gemm_w4_kernel), the
+    8-wave kernel forced (knob 0), the 4-wave kernel forced (1) and the 4-wave kernel's alternative tile order (2)."""
+    from cram_amd import _lib
+    prev = _lib.set_knob(_lib.KNOB_GEMM_VARIANT, {"auto": -1, "8wave": 0, "w4": 1, "w4_alt_order": 2}[request.param])
+    yield request.param
+    _lib.set_knob(_lib.KNOB_GEMM_VARIANT, prev)
+
+
 def _ulp(x: torch.Tensor, dtype) -> torch.Tensor:
     """ulp of the model dtype at |x| (float32 tensor)."""
     mant = 7 if dtype == torch.bfloat16 else 10
@@ -34,7 +44,7 @@ def _operands(M, N, K, dtype, dev, seed):
     (1, 256, 64), (77, 512, 128), (256, 256, 192), (300, 768, 4096), (1000, 1024, 320), (2048, 2048, 1024),
     (4097, 1536, 4096), (513, 256, 14336),
 ])
-def test_gemm_store_matches_fp32(gpu_device, dtype, M, N, K):
+def test_gemm_store_matches_fp32(gpu_device, gemm_variant, dtype, M, N, K):
     x, w = _operands(M, N, K, dtype, gpu_device, 7 * M + N + K)
     out = ops.gemm(x, w)
     ref = x.float() @ w.float().t()
@@ -49,7 +59,7 @@ def test_gemm_store_matches_fp32(gpu_device, dtype, M, N, K):
     assert exact >= 0.99, exact
 
 
-def test_gemm_strided_rows_and_tail(gpu_device):
+def test_gemm_strided_rows_and_tail(gpu_device, gemm_variant):
     """Row strides wider than K (views into fused buffers) and M not a multiple of the 256-row tile; rows past M
     stay untouched."""
     M, N, K = 333, 512, 256
@@ -72,7 +82,7 @@ def _silu_mul_expected(g32, u32, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("M,F,K", [(1, 128, 64), (300, 256, 512), (1111, 384, 4096), (2048, 1024, 1024)])
-def test_gemm_silu_mul_epilogue(gpu_device, dtype, M, F, K):
+def test_gemm_silu_mul_epilogue(gpu_device, gemm_variant, dtype, M, F, K):
     x, wgu = _operands(M, 2 * F, K, dtype, gpu_device, 3 * M + F + K)
     wil = ops.interleave_gate_up(wgu, F)
     out = ops.gemm(x, wil, ops.GEMM_SILU_MUL)
@@ -150,3 +160,36 @@ def test_gemm_splitk_silu_mul_cat(gpu_device, dtype, M, F, K, splits):
     # 4 ulp, >= 99 % within 1 (M = 1 has only 128 elements)
     assert (d <= 4 * _ulp(exp.float(), dtype) + 1e-6).all(), float((d / _ulp(exp.float(), dtype)).max())
     assert (d <= _ulp(exp.float(), dtype) + 1e-6).float().mean().item() >= 0.99
+
+
+def test_engine_fused_mlp_matches_library_pair(gpu_device):
+    """CrAMEngine.mlp at sweep row counts (gate/up on gemm_w4_kernel with the SiLU-mul epilogue, the interleaved
+    weight built from the checkpoint's [gate; up]) == hipBLASLt gate/up + cram_silu_mul within the bf16 noise of two
+    GEMM accumulation orders; an in-place weight edit (tests/planted.py does this) rebuilds the interleaved copy."""
+    from cram_amd import engine as E
+    sp = E.ModelSpec(1, 1024, 8, 2, 128, 1536, 1000, 1e-5, False)
+    eng = E.CrAMEngine.random(sp, gpu_device, seed=11, std=0.03)
+    lw = eng.layers[0]
+    x = (torch.randn(4608, sp.hidden, device=gpu_device, generator=torch.Generator(device=gpu_device).manual_seed(2))
+         ).to(torch.bfloat16)
+    assert eng._fused_mlp_ok(x)
+    fused = eng.mlp(x, lw)
+    prev = E.FUSED_MLP
+    E.FUSED_MLP = False
+    try:
+        lib = eng.mlp(x, lw)
+    finally:
+        E.FUSED_MLP = prev
+    d = (fused.float() - lib.float()).abs()
+    scale = lib.float().abs().mean().item()
+    assert d.max().item() <= 0.05 * lib.float().abs().max().item() and d.mean().item() <= 0.01 * scale, (d.max(), scale)
+    lw.wgu[:, :7] = 0                                            # in place: the interleaved copy must follow
+    E.FUSED_MLP = False
+    try:
+        lib2 = eng.mlp(x, lw)
+    finally:
+        E.FUSED_MLP = prev
+    fused2 = eng.mlp(x, lw)
+    d2 = (fused2.float() - lib2.float()).abs()
+    assert d2.mean().item() <= 0.01 * lib2.float().abs().mean().item()
+    assert not torch.equal(fused2, fused)

@@ -1,5 +1,6 @@
 """Decode-step projection GEMMs at the batch's row count (M = 256 rows at config 2, 16 at config 5): hipBLASLt via
-F.linear (default pick, and the decode pins of gemm_tune) against cram_gemm_splitk at several split counts.
+F.linear (default pick, and the decode pins of gemm_tune) against cram_gemm_splitk at several split counts and the
+one-pass 4-wave cram_gemm (gemm_w4_kernel; gate/up with its fused SiLU-mul, against hipBLASLt + cram_silu_mul).
 
 Weights are cycled through enough copies to exceed the 256 MB Infinity Cache, so every call streams its weight from
 HBM as the decode step does (each layer's weights are read once per step).  Prints one JSON line per (shape, method):
@@ -14,7 +15,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from cram_amd import gemm_tune, ops  # noqa: E402
+from cram_amd import _lib, gemm_tune, ops  # noqa: E402
 from cram_amd.engine import ModelSpec  # noqa: E402
 
 
@@ -81,6 +82,25 @@ def main():
                     err = float((out.float() - ops.silu_mul(ref.to(torch.bfloat16), F).float()).abs().max())
                 t = timeit(fn, ws_)
                 res.append((f"splitk{s}", t, err))
+        if ntiles and K % 64 == 0 and K // 64 >= 2:
+            # one-pass cram_gemm on the 4-wave kernel (gemm_w4_kernel); gate/up on the interleaved weight with the
+            # fused SiLU-mul epilogue
+            prev = _lib.set_knob(_lib.KNOB_GEMM_VARIANT, 1)
+            try:
+                if name == "gate_up":
+                    wil = [ops.interleave_gate_up(w, F) for w in ws_]
+                    fn = lambda w: ops.gemm(x, w, ops.GEMM_SILU_MUL)
+                    out = fn(wil[0])
+                    err = float((out.float() - ops.silu_mul(ref.to(torch.bfloat16), F).float()).abs().max())
+                    t = timeit(fn, wil)
+                    del wil
+                else:
+                    fn = lambda w: ops.gemm(x, w)
+                    err = float((fn(ws_[0]).float() - ref).abs().max())
+                    t = timeit(fn, ws_)
+            finally:
+                _lib.set_knob(_lib.KNOB_GEMM_VARIANT, prev)
+            res.append(("w4", t, err))
         for r in res:
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "method": r[0], "us": round(r[1], 2),
                               "weight_TBps": round(wbytes / r[1] / 1e6, 3),

@@ -55,11 +55,15 @@ def dma(kind, i):
 def dma_group(kind):
     """8 pieces of one operand: m0 set in an earlier gap, stepped 1 KiB after every piece (an MFMA always sits between
     an m0 write and the piece that reads it); then the destination toggles to the other stage, and after the
-    weight group (the second of a tile) the K offset moves to the next tile."""
+    weight group (the second of a tile) the K offset moves to the next tile, wrapping at the end of the K range (the
+    workgroup's K loop starts at a staggered tile: %[so] starts there, %[kend] = the range's bytes per row)."""
     out = [[f"s_mov_b32 m0, %[m{kind}]"]]
     for i in range(8):
         out.append([dma(kind, i)] + ([f"s_add_u32 m0, m0, 1024"] if i < 7 else []))
-    out.append([f"s_xor_b32 %[m{kind}], %[m{kind}], 0x10000"] + (["s_add_u32 %[so], %[so], 128"] if kind == "x" else []))
+    tail = [f"s_xor_b32 %[m{kind}], %[m{kind}], 0x10000"]
+    if kind == "x":
+        tail += ["s_add_u32 %[so], %[so], 128", "s_cmp_eq_u32 %[so], %[kend]", "s_cselect_b32 %[so], 0, %[so]"]
+    out.append(tail)
     return out
 
 
@@ -79,9 +83,8 @@ VENDOR = dict(
     NEXT_Y0=[93, 94, 95, 97, 98, 102, 103, 104],               # next tile's k-step 0 fragments
     NEXT_X0=[105, 106, 109, 112, 114, 117, 120, 123],
     LGKM_END=126)
-# every piece of tile t + 2 issued before B3 (the data B3 waits for was issued >= 1 1/4 tiles earlier)
-EARLY = dict(VENDOR, XDMA=[60, 61, 64, 67, 70, 73, 76, 79, 82, 85], LATE=0)
-VARIANTS = {"A": VENDOR, "B": EARLY}
+# (variant B: every piece of tile t + 2 before B3 -- measured 0.95-0.97x of A, r04; dropped)
+VARIANTS = {"A": VENDOR}
 
 
 def body(dma_on: bool, next_on: bool, c=VENDOR):
@@ -153,7 +156,7 @@ def emit():
         out.append(f"// variant {name}")
         out.append(f"#define CRAM_GEMM_W4_LOOP_{name}(TY) \\")
         put(prologue())
-        put(["s_cmp_eq_u32 %[n], 0", "s_cbranch_scc1 2f", "1:"])
+        put(["s_cmp_eq_u32 %[n], 0", "s_cbranch_scc1 2f", "1:"])   # (the wrap's s_cmp sits before this one)
         put(full)
         put(["s_sub_u32 %[n], %[n], 1", "s_cmp_eq_u32 %[n], 0", "s_cbranch_scc0 1b", "2:"])
         put(nodma)

@@ -44,7 +44,7 @@ for step in "$@"; do
                python3 tools/pmc_to_json.py $O/pmc $O/attn_pmc.json > /dev/null; cat $O/pmc_summary.txt ;;
     test:*)    k=${step#test:}; n=$(echo "$k" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
                timeout -k 10 900 $PYT -x -v -s -k "$k" > $O/test_$n.txt 2>&1; tail -3 $O/test_$n.txt ;;
-    py:*)      a=${step#py:}; n=$(basename "${a%%,*}" .py)
+    py:*)      a=${step#py:}; n=$(basename "${a%%,*}" .py)$(echo "${a#*,}" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
                timeout -k 10 600 python -u ${a//,/ } > $O/$n.txt 2>&1; tail -30 $O/$n.txt ;;
     *)         echo "unknown step $step"; exit 2 ;;
   esac
