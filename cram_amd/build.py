@@ -82,7 +82,7 @@ def _build(objdir: Path, verbose: bool) -> Path:
     for src in SOURCES:
         obj = objdir / (src.name + ".o")
         # the attention library keeps its device assembly (same compile as the object) for the register audit
-        extra = ["-save-temps=obj"] if src.name == "cram_attn.hip" else []
+        extra = ["-save-temps=obj"] if src.name in ASM_SOURCES else []
         cmd = common + extra + ["-c", str(src), "-o", str(obj)]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
@@ -91,7 +91,7 @@ def _build(objdir: Path, verbose: bool) -> Path:
     failed = [cmd for p, cmd in procs if p.wait() != 0]
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
-    asm = x64_asm_path().read_text()
+    asm = "\n".join(asm_path(src).read_text() for src in ASM_SOURCES)
     for kname in ASM_KERNELS:
         bad = audit_asm_kernel(asm, kname)
         if bad:
@@ -108,15 +108,24 @@ def _build(objdir: Path, verbose: bool) -> Path:
 
 
 def device_asm(out_dir: Path) -> str:
-    """Device assembly of cram_attn.hip compiled with the library's flags into out_dir (for the register audit
-    without touching the installed library): the saved assembly of the last build when it matches the sources."""
-    saved, stamp = x64_asm_path(), PKG_DIR / "build" / "asm.hash"
-    if saved.exists() and stamp.exists() and stamp.read_text().strip() == source_hash():
-        return saved.read_text()
-    out = Path(out_dir) / "cram_attn.s"
-    subprocess.run([_hipcc(), f"--offload-arch={ARCH}", *COMMON_FLAGS, "-I", str(REPO_DIR / "include"),
-                    "--cuda-device-only", "-S", str(CSRC / "cram_attn.hip"), "-o", str(out)], check=True)
-    return out.read_text()
+    """Device assembly of the sources with register-owning kernels (ASM_SOURCES), compiled with the library's flags
+    into out_dir (for the register audit without touching the installed library): the saved assembly of the last
+    build when it matches the sources."""
+    stamp = PKG_DIR / "build" / "asm.hash"
+    if stamp.exists() and stamp.read_text().strip() == source_hash() and all(asm_path(s).exists() for s in ASM_SOURCES):
+        return "\n".join(asm_path(s).read_text() for s in ASM_SOURCES)
+    texts = []
+    for src in ASM_SOURCES:
+        out = Path(out_dir) / (src + ".s")
+        subprocess.run([_hipcc(), f"--offload-arch={ARCH}", *COMMON_FLAGS, "-I", str(REPO_DIR / "include"),
+                        "--cuda-device-only", "-S", str(CSRC / src), "-o", str(out)], check=True)
+        texts.append(out.read_text())
+    return "\n".join(texts)
+
+
+def asm_path(src: str) -> Path:
+    """Device assembly of a source saved by the last build (-save-temps=obj)."""
+    return PKG_DIR / "build" / f"{src.rsplit('.', 1)[0]}-hip-amdgcn-amd-amdhsa-{ARCH}.s"
 
 
 def kernel_source_hash() -> str:
@@ -132,7 +141,7 @@ def kernel_source_hash() -> str:
 
 def x64_asm_path() -> Path:
     """Device assembly of cram_attn.hip saved by the last build (-save-temps=obj)."""
-    return PKG_DIR / "build" / f"cram_attn-hip-amdgcn-amd-amdhsa-{ARCH}.s"
+    return asm_path("cram_attn.hip")
 
 
 def kernel_body(asm: str, name: str) -> str:
@@ -155,7 +164,10 @@ _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "
 
 # kernels that own accumulator registers by name inside their inline asm (x64: O = a[0:127], Q = a[128:191];
 # x32: O = a[0:63], Q = a[64:95])
-ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernel")
+# (gemm_w4_kernel: all 256 accumulators a[0:255], its K loop one asm statement, the epilogue's accumulator reads
+# separate statements -- nothing of hipcc's may touch an AGPR in between; both instantiations are audited)
+ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernel", "gemm_w4_kernelIDF16bLi0E", "gemm_w4_kernelIDF16bLi1E")
+ASM_SOURCES = ("cram_attn.hip", "cram_gemm.hip")
 
 
 def audit_asm_kernel(asm: str, kname: str = "prefill_x32_kernel") -> list:

@@ -381,30 +381,24 @@ __device__ __forceinline__ u32x4 w4_srd(const void* base, uint32_t bytes) {
 // tile order of the 4-wave kernel: the XCD-bijective remap of tile_of, then groups of 8 weight tiles (activation
 // tiles innermost) or of 8 activation tiles (weight tiles innermost); measured alternatives (r04, tools/gemm_ab_knob.py):
 // groups of 16 weight tiles 0.92-0.95x, no XCD remap 0.86-0.95x
-__device__ __forceinline__ void tile_of_w4(const GemmParams& p, int bid, int& tm, int& tn) {
+__device__ __forceinline__ int2 tile_of_w4(const GemmParams& p, int bid) {     // (tm, tn)
   const int xcd = bid & 7, q8 = p.nblocks >> 3, r8 = p.nblocks & 7;
   const int wid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   constexpr int G = 8;
-  if (p.raster == 2) {                           // groups of 8 activation tiles, weight tiles innermost
-    const int grp = wid / (G * p.ntn);
-    const int gw = min(G, p.ntm - grp * G);
-    const int rem = wid - grp * G * p.ntn;
-    tm = grp * G + rem % gw;
-    tn = rem / gw;
-  } else {                                       // groups of 8 weight tiles, activation tiles innermost
-    const int grp = wid / (G * p.ntm);
-    const int gw = min(G, p.ntn - grp * G);
-    const int rem = wid - grp * G * p.ntm;
-    tn = grp * G + rem % gw;
-    tm = rem / gw;
-  }
+  const bool by_m = p.raster == 2;               // groups of 8 activation tiles, weight tiles innermost
+  const int nmaj = by_m ? p.ntm : p.ntn, nmin = by_m ? p.ntn : p.ntm;
+  const int grp = wid / (G * nmin);
+  const int gw = min(G, nmaj - grp * G);
+  const int rem = wid - grp * G * nmin;
+  const int major = grp * G + rem % gw, minor = rem / gw;
+  return by_m ? make_int2(major, minor) : make_int2(minor, major);
 }
 
 template <typename T, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[W4_LDS];
-  int tm, tn;
-  tile_of_w4(p, blockIdx.x, tm, tn);
+  const int2 tt = tile_of_w4(p, blockIdx.x);
+  const int tm = tt.x, tn = tt.y;
   const int n0 = tn * BN, m0 = tm * BM;
   const int kc = p.kts * BK;
   const int tid = threadIdx.x, lane = tid & 63;
