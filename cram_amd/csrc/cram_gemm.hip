@@ -326,6 +326,9 @@ __global__ __launch_bounds__(512) void gemm_tn_kernel(GemmParams p) {
 #include "gemm_w4_loop.inc"
 
 constexpr int W4_LDS = 2 * 65536;              // two stages of (weight image 32 KiB | activation image 32 KiB)
+#ifdef CRAM_W4_STAMPS
+__device__ unsigned* g_w4_stamps;              // [block][wave][5] (diagnostic build only)
+#endif
 
 #define CRAM_V128_255_CLOBBERS                                                                                       \
   "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141",    \
@@ -411,18 +414,19 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   // rows live in the per-lane voffset (range-checked: a row at or past M reads zeros), the K-tile in soffset
   u32x4 sx = w4_srd(xb, (uint32_t)((BN - 1) * p.ldx * 2 + kc * 2));
   u32x4 sy = w4_srd(yb, (uint32_t)((yrows - 1) * p.ldy * 2 + kc * 2));
-  // LDS-DMA piece i of this wave: image rows 64 wave + 8 i .. +7; lane L fetches row + L / 8, chunk (L % 8) ^ swz(row)
+  // LDS-DMA piece i of this wave: image rows 32 i + 8 wave .. +7 (the 4 waves' i-th pieces cover 32 adjacent rows);
+  // lane L fetches row + L / 8, chunk (L % 8) ^ swz(row)
   uint32_t vx[8], vy[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int row = 64 * wave + 8 * i + (lane >> 3);
+    const int row = 32 * i + 8 * wave + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     vx[i] = (uint32_t)(row * p.ldx * 2 + c * 16);
     vy[i] = (uint32_t)(row * p.ldy * 2 + c * 16);
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
-  uint32_t mx = __builtin_amdgcn_readfirstlane(lds0 + 8192 * wave);
-  uint32_t my = __builtin_amdgcn_readfirstlane(lds0 + 32768 + 8192 * wave);
+  uint32_t mx = __builtin_amdgcn_readfirstlane(lds0 + 1024 * wave);
+  uint32_t my = __builtin_amdgcn_readfirstlane(lds0 + 32768 + 1024 * wave);
   // K offset of the next tile to stage (soffset); kend wraps it (the generated loop supports a rotated K start: a
   // staggered start per workgroup measured 0.97-0.99x, r04, so every workgroup starts at tile 0)
   uint32_t so = 0;
@@ -448,47 +452,90 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
                  [vy1] "v"(vy[1]), [vy2] "v"(vy[2]), [vy3] "v"(vy[3]), [vy4] "v"(vy[4]), [vy5] "v"(vy[5]),           \
                  [vy6] "v"(vy[6]), [vy7] "v"(vy[7])                                                                  \
                : "memory", "scc", CRAM_V128_255_CLOBBERS, CRAM_A256_CLOBBERS)
+#ifndef CRAM_W4_STAMPS
   if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "bf16");
   else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "f16");
+#else
+  // diagnostic build (tools/w4_stamps.hip): the stamped stream, its per-wave cycle sums (B1, B2, B3, whole tiles,
+  // tile count) written to g_w4_stamps -- a buffer of its own, never an output element
+  uint32_t st0, st1, st2, st3, st4;
+  asm volatile("s_mov_b32 %[keep], m0\n\t"
+               "v_accvgpr_write_b32 a0, 0\n\t.set cram_w4i, 1\n\t.rept 255\n\t"
+               "v_accvgpr_write_b32 a[cram_w4i], 0\n\t.set cram_w4i, cram_w4i+1\n\t.endr\n\t"
+               CRAM_GEMM_W4_LOOP_S("bf16")
+               "s_mov_b32 m0, %[keep]\n\t"
+               "v_mov_b32 %[st0], s80\n\tv_mov_b32 %[st1], s81\n\tv_mov_b32 %[st2], s82\n\t"
+               "v_mov_b32 %[st3], s83\n\tv_mov_b32 %[st4], s84"
+               : [keep] "=&s"(keep), [rx0] "+v"(rx0), [rx1] "+v"(rx1), [ry0] "+v"(ry0), [ry1] "+v"(ry1),
+                 [mx] "+s"(mx), [my] "+s"(my), [so] "+s"(so), [n] "+s"(n), [st0] "=&v"(st0), [st1] "=&v"(st1),
+                 [st2] "=&v"(st2), [st3] "=&v"(st3), [st4] "=&v"(st4)
+               : [sx] "s"(sx), [sy] "s"(sy), [kend] "s"(kend), [vx0] "v"(vx[0]), [vx1] "v"(vx[1]), [vx2] "v"(vx[2]),
+                 [vx3] "v"(vx[3]), [vx4] "v"(vx[4]), [vx5] "v"(vx[5]), [vx6] "v"(vx[6]), [vx7] "v"(vx[7]),
+                 [vy0] "v"(vy[0]), [vy1] "v"(vy[1]), [vy2] "v"(vy[2]), [vy3] "v"(vy[3]), [vy4] "v"(vy[4]),
+                 [vy5] "v"(vy[5]), [vy6] "v"(vy[6]), [vy7] "v"(vy[7])
+               : "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
+                 "s92", "s93", "s94", "s95", CRAM_V128_255_CLOBBERS, CRAM_A256_CLOBBERS);
+  if (lane == 0) {
+    unsigned* o = g_w4_stamps + ((size_t)blockIdx.x * 4 + wave) * 5;
+    o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st4;
+  }
+#endif
 #undef CRAM_W4_ASM
 
-  // epilogue: lane (r, g) holds acc tile (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]
-  const int mrow = m0 + 128 * wm + fr;
-  const int ncol = n0 + 128 * wn + 4 * fg;
+  // epilogue through LDS (the output stage of the guide's T21: row-contiguous 16-byte stores instead of 64 scattered
+  // 8-byte stores per lane -- the 8-byte form left each workgroup a long store-issue tail).  Lane (r, g) holds acc tile
+  // (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]; each wave rounds its 128 rows (256 B each, or 128 B of SiLU-mul
+  // output) into its own 32 KiB of the (now idle) ring, 8-byte units swizzled by row so a ds_write lane group spreads
+  // over the banks, then reads back whole 16-byte row pieces and stores them.
+  __syncthreads();                               // every wave's last fragment reads are done (no LDS-DMA is pending)
   using V4 = typename GVec<T>::x4;
-  T* ob = static_cast<T*>(p.out);
+  using V8 = typename GVec<T>::x8;
+  constexpr int RB = EPI == CRAM_GEMM_STORE ? 256 : 128;      // staged bytes per row
+  char* const wl = smem + wave * 32768;
+  auto swz = [](int row) { return RB == 256 ? (row & 7) << 2 : ((row >> 1) & 3) << 2; };   // unit XOR (bits 2..4)
   static_for<8>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
-    const int m = mrow + 16 * b;
-    if (m < p.M) {
-      if constexpr (EPI == CRAM_GEMM_STORE) {
-        static_for<8>([&](auto ai) {
-          constexpr int a = decltype(ai)::value;
-          const f32x4 v = acc4<4 * (8 * a + b)>();
-          V4 o;
+    const int ml = 16 * b + fr;                  // the lane's row within the wave's 128
+    const int sw = swz(ml);
+    if constexpr (EPI == CRAM_GEMM_STORE) {
+      static_for<8>([&](auto ai) {
+        constexpr int a = decltype(ai)::value;
+        const f32x4 v = acc4<4 * (8 * a + b)>();
+        V4 o;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = (T)v[i];
-          *reinterpret_cast<V4*>(ob + (int64_t)m * p.ldo + ncol + 16 * a) = o;
-        });
-      } else {
-        // gate tiles a = 0, 1, 4, 5 and their up tiles a + 2 (weight rows interleaved in blocks of 32): gate column
-        // n' = n + 16 a is output column f = 32 (n' / 64) + n' % 64
-        static_for<4>([&](auto ji) {
-          constexpr int a = (decltype(ji)::value & 1) + 4 * (decltype(ji)::value >> 1);
-          const f32x4 gv = acc4<4 * (8 * a + b)>(), uv = acc4<4 * (8 * (a + 2) + b)>();
-          const int ng = ncol + 16 * a;
-          const int f = 32 * (ng >> 6) + (ng & 63);
-          V4 o;
+        for (int i = 0; i < 4; ++i) o[i] = (T)v[i];
+        *reinterpret_cast<V4*>(wl + ml * RB + (((4 * a + fg) ^ sw) * 8)) = o;
+      });
+    } else {
+      // gate tiles a = 0, 1, 4, 5 and their up tiles a + 2 (weight rows interleaved in blocks of 32): the wave's
+      // output columns are f = 32 (a >> 2) + 16 (a & 1) + 4 g + i of its 64
+      static_for<4>([&](auto ji) {
+        constexpr int a = (decltype(ji)::value & 1) + 4 * (decltype(ji)::value >> 1);
+        const f32x4 gv = acc4<4 * (8 * a + b)>(), uv = acc4<4 * (8 * (a + 2) + b)>();
+        V4 o;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float g = rnd<T>(gv[i]), u = rnd<T>(uv[i]);
-            o[i] = (T)(rnd<T>(g / (1.0f + expf(-g))) * u);
-          }
-          *reinterpret_cast<V4*>(ob + (int64_t)m * p.ldo + f) = o;
-        });
-      }
+        for (int i = 0; i < 4; ++i) {
+          const float g = rnd<T>(gv[i]), u = rnd<T>(uv[i]);
+          o[i] = (T)(rnd<T>(g / (1.0f + expf(-g))) * u);
+        }
+        const int unit = 8 * (a >> 2) + 4 * (a & 1) + fg;
+        *reinterpret_cast<V4*>(wl + ml * RB + ((unit ^ sw) * 8)) = o;
+      });
     }
   });
+  // each wave reads back only its own rows: its writes are ordered before its reads (no barrier needed)
+  constexpr int LPR = RB / 16;                   // lanes per row: 16 | 8
+  constexpr int RPI = 64 / LPR;                  // rows per instruction: 4 | 8
+  const int cl = lane % LPR, rl = lane / LPR;
+  T* ob = static_cast<T*>(p.out);
+  const int64_t col0 = EPI == CRAM_GEMM_STORE ? (int64_t)n0 + 128 * wn + 8 * cl : (int64_t)(n0 / 2) + 64 * wn + 8 * cl;
+#pragma unroll 4
+  for (int j = 0; j < 128 / RPI; ++j) {
+    const int ml = RPI * j + rl;
+    const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
+    const int m = m0 + 128 * wm + ml;
+    if (m < p.M) *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + col0) = v;
+  }
 }
 
 // Split-K combine: out = epilogue(sum over the K ranges of the fp32 partials [splits][M][N], in range order — the
@@ -569,10 +616,11 @@ extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx,
   const dim3 g(p.nblocks);
   int kv = -1;
   cram_get_knob(CRAM_KNOB_GEMM_VARIANT, &kv);
-  // knob 1 / -1: the 4-wave kernel, tile order by weight-tile groups (best for gate/up and down); 2: activation-tile
-  // groups (A/B; 1.00-1.03x on q/k/v and o_proj, 0.94x on down, r04)
-  p.raster = kv == 2 ? 2 : 0;
-  if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && kv != 0) {
+  // tile order of the 4-wave kernel: groups of 8 activation tiles for short, narrow GEMMs (q/k/v, o_proj: N <= 6144,
+  // K <= 4096: 1.02-1.03x the other order), groups of 8 weight tiles otherwise (down_proj: 1.07x; gate/up: equal)
+  // (tools/gemm_ab_knob.py, r04); knob 2 forces the activation-tile groups, 1 the weight-tile groups (A/B)
+  p.raster = kv == 2 ? 2 : (kv == 1 ? 0 : ((N <= 6144 && K <= 4096) ? 2 : 0));
+  if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && (ldo & 7) == 0 && kv != 0) {   // (16-byte output rows)
     if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE>), g, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL>), g, dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;

@@ -73,9 +73,10 @@ int cram_abi_version(void);
  *                              per wave, hand-ordered stream (bf16, d = 128, GQA groups of 4k; otherwise as 0)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
- *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles on the 4-wave 128 x 128-per-wave
- *                              kernel (1), others on the 8-wave kernel (0); 0 / 1 force one (1 falls back to 0 where
- *                              it does not apply); 2 = the 4-wave kernel with its alternative tile order (A/B)
+ *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles and 16-byte output rows on the
+ *                              4-wave 128 x 128-per-wave kernel (tile order by shape), others on the 8-wave kernel;
+ *                              0 = the 8-wave kernel; 1 / 2 = the 4-wave kernel with weight-tile / activation-tile
+ *                              groups (where it applies; otherwise as 0)
  * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob stores the value in
  * *value and returns CRAM_OK, or CRAM_ERR_INVALID_ARG for an unknown knob / null pointer (ABI 4: the value -1,
  * "automatic", is never an error code).
