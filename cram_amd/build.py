@@ -18,7 +18,7 @@ REPO_DIR = PKG_DIR.parent
 CSRC = PKG_DIR / "csrc"
 LIB_PATH = PKG_DIR / "libcram_attn.so"
 SOURCES = [CSRC / "cram_attn.hip", CSRC / "cram_fused.hip", CSRC / "cram_gemm.hip", CSRC / "cram_spans.cpp"]
-HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc",
+HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_asm.inc", CSRC / "prefill_x32.inc",
            CSRC / "gemm_w4_loop.inc"]
 ARCH = "gfx950"
 
@@ -129,12 +129,12 @@ def asm_path(src: str) -> Path:
 
 
 def kernel_source_hash() -> str:
-    """Identity of the attention kernels' source (cram_attn.hip, prefill_x64.inc, prefill_x32.inc, the ABI header):
+    """Identity of the attention kernels' source (cram_attn.hip, prefill_asm.inc, prefill_x32.inc, the ABI header):
     PMC evidence (profiles/attn_pmc.json) records the hash it was measured on, and bench.py uses it only while it
     matches."""
     import hashlib
     h = hashlib.sha256()
-    for f in (CSRC / "cram_attn.hip", CSRC / "prefill_x64.inc", CSRC / "prefill_x32.inc", REPO_DIR / "include" / "cram_attn.h"):
+    for f in (CSRC / "cram_attn.hip", CSRC / "prefill_asm.inc", CSRC / "prefill_x32.inc", REPO_DIR / "include" / "cram_attn.h"):
         h.update(f.read_bytes())
     return h.hexdigest()[:16]
 
@@ -162,17 +162,16 @@ def _sgprs(op: str) -> set:
 _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "s_barrier", "s_setprio", "s_endpgm")
 
 
-# kernels that own accumulator registers by name inside their inline asm (x64: O = a[0:127], Q = a[128:191];
-# x32: O = a[0:63], Q = a[64:95])
-# (gemm_w4_kernel: all 256 accumulators a[0:255], its K loop one asm statement, the epilogue's accumulator reads
-# separate statements -- nothing of hipcc's may touch an AGPR in between; both instantiations are audited)
-ASM_KERNELS = ("prefill_x64_kernel", "prefill_x32_kernel", "gemm_w4_kernelIDF16bLi0E", "gemm_w4_kernelIDF16bLi1E")
+# kernels that own accumulator registers by name inside their inline asm: prefill_x32_kernel (O = a[0:63],
+# Q = a[64:95]) and gemm_w4_kernel (all 256 accumulators a[0:255], its K loop one asm statement, the epilogue's
+# accumulator reads separate statements -- nothing of hipcc's may touch an AGPR in between; both instantiations)
+ASM_KERNELS = ("prefill_x32_kernel", "gemm_w4_kernelIDF16bLi0E", "gemm_w4_kernelIDF16bLi1E")
 ASM_SOURCES = ("cram_attn.hip", "cram_gemm.hip")
 
 
 def audit_asm_kernel(asm: str, kname: str = "prefill_x32_kernel") -> list:
-    """The kernels of ASM_KERNELS own accumulator registers by name inside their inline asm (prefill_x64_kernel:
-    O = a[0:127], Q = a[128:191]; prefill_x32_kernel: O = a[0:63], Q = a[64:95]); hipcc knows nothing of that.
+    """The kernels of ASM_KERNELS own accumulator registers by name inside their inline asm (prefill_x32_kernel:
+    O = a[0:63], Q = a[64:95]; gemm_w4_kernel: a[0:255]); hipcc knows nothing of that.
     Returns the violations in kernel `kname` (empty = clean):
       * any v_accvgpr_* / AGPR operand the COMPILER emitted (outside the kernel's ;;#ASMSTART..;;#ASMEND blocks);
       * any scratch traffic in the kernel;
@@ -214,7 +213,7 @@ def audit_asm_kernel(asm: str, kname: str = "prefill_x32_kernel") -> list:
     return bad
 
 
-audit_x64 = audit_asm_kernel          # the round-2 name (x64 was the first such kernel)
+audit_x64 = audit_asm_kernel          # the round-2 name
 
 
 if __name__ == "__main__":

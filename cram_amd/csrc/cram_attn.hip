@@ -588,8 +588,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
                      static_cast<T*>(p.o) + b * p.o_sb + tok0 * p.o_st + hq * p.o_sh, p.o_st, q_row0, Tq);
 }
 
-// one-wave-per-SIMD prefill (64 rows per wave, hand-ordered MFMA / softmax stream): prefill_x64_kernel
-#include "prefill_x64.inc"
+// register-pinned asm helpers of the hand-scheduled prefill (prefill_asm.inc) and the kernel (prefill_x32.inc)
+#include "prefill_asm.inc"
 // two workgroups per CU, 32 rows per wave, the same hand-ordered stream: prefill_x32_kernel
 #include "prefill_x32.inc"
 
@@ -1039,7 +1039,7 @@ inline void knobs_init() {
   std::call_once(g_knob_once, [] {
     const char* e = getenv("CRAM_PREFILL_VARIANT");
     g_knob[CRAM_KNOB_PREFILL_VARIANT].store(
-        (e && (e[0] == '0' || e[0] == '3' || e[0] == '4' || e[0] == '6' || e[0] == '7' || e[0] == '8')) ? e[0] - '0'
+        (e && (e[0] == '0' || e[0] == '3' || e[0] == '4' || e[0] == '7' || e[0] == '8')) ? e[0] - '0'
                                                                                                   : -1);
     const char* eu = getenv("CRAM_DECODE_U");
     g_knob[CRAM_KNOB_DECODE_U].store((eu && (eu[0] == '1' || eu[0] == '2' || eu[0] == '4')) ? eu[0] - '0' : -1);
@@ -1071,24 +1071,10 @@ int launch_prefill(PrefillParams& p, hipStream_t stream) {
   // 544 TFLOP/s, but B = 1 x T = 8300 582 vs 807 (one 7-wave workgroup per CU instead of two 4-wave ones;
   // tools/ab_prefill_inproc.py, profiles/r02/ab_prefill_hp7.log).  Knob 0 forces the 4-wave layout.
   const int kv = knob(CRAM_KNOB_PREFILL_VARIANT);
-  // variant 6: prefill_x64_kernel (one wave per SIMD, 64 rows per wave; bf16, d = 128, GQA groups of 4k): opt-in since
-  // variant 4 matches it at 8.3k tokens and wins below (x64 runs 0.80-0.89x at the IE-sweep shape, B = 33 x T = 962:
-  // nothing hides its per-block prologue and store tail)
-  if constexpr (D == 128 && std::is_same<T, __bf16>::value) {
-    if (kv == 6 && G % 4 == 0) {
-      p.hp = 4;
-      p.nqb = (p.Tq + 63) / 64;
-      const int64_t nb = (int64_t)p.nqb * (p.Hq / 4) * p.B;
-      if (nb > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
-      p.nblocks = (int)nb;
-      hipLaunchKernelGGL(prefill_x64_kernel, dim3(p.nblocks), dim3(256), 0, stream, p);
-      return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
-    }
-  }
-  // variant 4: prefill_x32_kernel (two workgroups per CU, 32 rows per wave, x64's hand-ordered stream; bf16, d = 128,
-  // GQA groups of 4k).  Automatic from 256 query rows: 1.10-1.12x the 4-wave kernel at the IE-sweep shapes, 1.10x /
-  // 1.16x at 8.3k tokens unbiased / biased (= x64 / 1.08x x64), 1.06x at B = 3 x 517 biased; 0.94x on a B = 2 x 77
-  // call (tools/ab_x64.hip, profiles/r03/x32/)
+  // variant 4: prefill_x32_kernel (two workgroups per CU, 32 rows per wave, hand-ordered MFMA / softmax stream; bf16,
+  // d = 128, GQA groups of 4k).  Automatic from 256 query rows: 1.10-1.12x the 4-wave kernel at the IE-sweep shapes,
+  // 1.10x / 1.16x at 8.3k tokens unbiased / biased (1.08x round 2's one-wave-per-SIMD x64 kernel, removed in round 4),
+  // 1.06x at B = 3 x 517 biased; 0.94x on a B = 2 x 77 call (tools/ab_x32.hip, profiles/r03/x32/)
   if constexpr (D == 128 && std::is_same<T, __bf16>::value) {
     if ((kv == 4 || (kv == -1 && p.Tq >= 256)) && G % 4 == 0) {
       p.hp = 4;
@@ -1200,8 +1186,8 @@ int cram_abi_version(void) { return CRAM_ABI_VERSION; }
 int cram_set_knob(int which, int value) {
   if (which < 0 || which >= CRAM_KNOB_COUNT) return CRAM_ERR_INVALID_ARG;
   knobs_init();
-  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 4 && value != 6 &&
-      value != 7 && value != 8)
+  if (which == CRAM_KNOB_PREFILL_VARIANT && value != -1 && value != 0 && value != 3 && value != 4 && value != 7 &&
+      value != 8)
     return CRAM_ERR_INVALID_ARG;
   if (which == CRAM_KNOB_DECODE_U && value != -1 && value != 1 && value != 2 && value != 4)
     return CRAM_ERR_INVALID_ARG;

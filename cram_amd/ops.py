@@ -56,8 +56,6 @@ def prefill_kernel_name(dtype: str, Hq: int, Hkv: int, Tq: int, d: int = 128) ->
     kv = _lib.get_knob(_lib.KNOB_PREFILL_VARIANT)
     G = Hq // Hkv
     if d == 128 and dtype == "bf16" and G % 4 == 0:
-        if kv == 6:
-            return "prefill_x64_kernel"
         if kv == 4 or (kv == -1 and Tq >= 256):
             return "prefill_x32_kernel"
     if d == 128 and G % 7 == 0 and (kv == 7 or (kv == -1 and Tq <= 2048)):

@@ -68,9 +68,9 @@ int cram_abi_version(void);
  *   CRAM_KNOB_PREFILL_VARIANT  -1 = automatic: 64-key tiles, 4 waves, except GQA-7 groups with sequences <= 2048
  *                              (7-wave workgroups) and bf16 d = 128 GQA groups of 4k with >= 256 query rows (variant 4);
  *                              0 = always 4 waves; 3 = 32-key tiles; 8 = 8-wave workgroups;
- *                              7 = 7-wave workgroups for GQA-7 groups; 6 = one wave per SIMD, 64 rows per wave
- *                              (bf16, d = 128, GQA groups of 4k; otherwise as 0); 4 = two workgroups per CU, 32 rows
- *                              per wave, hand-ordered stream (bf16, d = 128, GQA groups of 4k; otherwise as 0)
+ *                              7 = 7-wave workgroups for GQA-7 groups; 4 = two workgroups per CU, 32 rows per wave,
+ *                              hand-ordered stream (bf16, d = 128, GQA groups of 4k; otherwise as 0).  (6, round 2's
+ *                              one-wave-per-SIMD kernel, was removed in round 4: CRAM_ERR_INVALID_ARG)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
  *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles and 16-byte output rows on the

@@ -23,15 +23,15 @@ def gpu_device():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=["bk64", "bk32", "w8", "hp7", "x64", "x32"])
+@pytest.fixture(params=["bk64", "bk32", "w8", "hp7", "x32"])
 def prefill_variant(request):
     """Run a prefill test on every d=128 prefill kernel: the 4-wave 64-key tiles at two waves per SIMD (variant 0), the
     opt-in 32-key tiles at three (variant 3), the 8-wave workgroups (variant 8), the 7-wave GQA-7 workgroups
-    (variant 7; the automatic choice for GQA-7 up to 2048 tokens) and the one-wave-per-SIMD kernel with 64 rows per
-    wave (variant 6: bf16 GQA groups of 4k; other shapes fall back to variant 0) and its two-workgroups-per-CU form with
-    32 rows per wave (variant 4, same eligibility), selected through the library's process-wide knob (cram_set_knob)."""
+    (variant 7; the automatic choice for GQA-7 up to 2048 tokens) and the hand-scheduled two-workgroups-per-CU kernel
+    with 32 rows per wave (variant 4: bf16 GQA groups of 4k, the automatic choice from 256 rows; other shapes fall
+    back to variant 0), selected through the library's process-wide knob (cram_set_knob)."""
     from cram_amd import _lib
-    prev = _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, {"bk64": 0, "bk32": 3, "w8": 8, "hp7": 7, "x64": 6, "x32": 4}[request.param])
+    prev = _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, {"bk64": 0, "bk32": 3, "w8": 8, "hp7": 7, "x32": 4}[request.param])
     yield request.param
     _lib.set_knob(_lib.KNOB_PREFILL_VARIANT, prev)
 

@@ -1,6 +1,6 @@
-"""prefill_x64_kernel owns accumulator registers by name (O = a[0:127], Q = a[128:191]), and so does
-prefill_x32_kernel (O = a[0:63], Q = a[64:95]); hipcc knows nothing of that ownership, so a compiler spill or copy into
-the AGPR file would silently corrupt O or Q.  cram_amd.build runs the audit
+"""prefill_x32_kernel owns accumulator registers by name (O = a[0:63], Q = a[64:95]), and so does gemm_w4_kernel
+(all of a[0:255]); hipcc knows nothing of that ownership, so a compiler spill or copy into the AGPR file would silently
+corrupt O, Q or the GEMM accumulators.  cram_amd.build runs the audit
 (cram_amd.build.audit_asm_kernel) on the device assembly of every build it makes and refuses to install a library that fails
 it; this CPU test re-checks the assembly of the current build: no v_accvgpr_* instruction or AGPR operand outside the
 kernel's own inline-asm statements, no scratch traffic, and 5 wait states between any VALU write of an LDS-DMA

@@ -1,10 +1,11 @@
-// A/B and agreement check of prefill_x64_kernel (one wave per SIMD, 64 rows per wave) and prefill_x32_kernel (two
-// workgroups per CU, 32 rows per wave) against the library's prefill_kernel on the same inputs, in one process:
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/ab_x64.hip -o tools/ab_x64 && tools/ab_x64
+// A/B and agreement check of prefill_x32_kernel (two workgroups per CU, 32 rows per wave) against the library's
+// prefill_kernel on the same inputs, in one process (arm "x32b" launches x32 again: the run-to-run noise of the A/B;
+// round 2's one-wave-per-SIMD x64 kernel held that arm until round 4 removed it):
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/ab_x32.hip -o tools/ab_x32 && tools/ab_x32
 // Cases: the IE-sweep shape (B=33, T=962, Llama-3 GQA 32/8, d 128, fused QKV layout), a suffix-style call (queries at
 // positions p0.., keys 0..p0+T), a biased call (some heads enabled, -inf and log 0.1 spans), the 8.3k-token prompt.
 // Prints max |x - library| and the kernels' times (median of 5 rounds of 10 launches each, interleaved).
-// -DCRAM_X64_STAMPS / -DCRAM_X32_STAMPS: per-phase cycle stamps of that kernel.
+// -DCRAM_X32_STAMPS: per-phase cycle stamps of the kernel.
 #include "../cram_amd/csrc/cram_attn.hip"
 
 #include <algorithm>
@@ -100,13 +101,13 @@ int main(int argc, char** argv) {
     p.cu = nullptr;
     PrefillParams p1 = p, p2 = p, p3 = p;
     p1.o = o1; p1.hp = 4; p1.nqb = (c.T + 31) / 32; p1.nblocks = p1.nqb * (c.Hq / 4) * c.B;
-    p2.o = o2; p2.hp = 4; p2.nqb = (c.T + 63) / 64; p2.nblocks = p2.nqb * (c.Hq / 4) * c.B;
+    p2.o = o2; p2.hp = 4; p2.nqb = (c.T + 31) / 32; p2.nblocks = p2.nqb * (c.Hq / 4) * c.B;
     p3.o = o3; p3.hp = 4; p3.nqb = (c.T + 31) / 32; p3.nblocks = p3.nqb * (c.Hq / 4) * c.B;
     auto run = [&](int which) {
       if (which == 0)
         hipLaunchKernelGGL((prefill_kernel<__bf16, 128, 64, 2>), dim3(p1.nblocks), dim3(256), 0, 0, p1);
       else if (which == 1)
-        hipLaunchKernelGGL(prefill_x64_kernel, dim3(p2.nblocks), dim3(256), 0, 0, p2);
+        hipLaunchKernelGGL(prefill_x32_kernel, dim3(p3.nblocks), dim3(256), 0, 0, p2);
       else
         hipLaunchKernelGGL(prefill_x32_kernel, dim3(p3.nblocks), dim3(256), 0, 0, p3);
     };
@@ -143,29 +144,6 @@ int main(int argc, char** argv) {
         t[w].push_back(ms / iters);
       }
     for (auto& x : t) std::sort(x.begin(), x.end());
-#ifdef CRAM_X64_STAMPS
-    {
-      unsigned long long* st;
-      const size_t ns = (size_t)p2.nblocks * 4 * 8;
-      CK(hipMalloc(&st, ns * 8));
-      CK(hipMemset(st, 0, ns * 8));
-      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_x64_stamps), &st, sizeof(st)));
-      run(1);
-      CK(hipDeviceSynchronize());
-      std::vector<unsigned long long> hs(ns);
-      CK(hipMemcpy(hs.data(), st, ns * 8, hipMemcpyDeviceToHost));
-      double sum[8] = {};
-      for (size_t w = 0; w < (size_t)p2.nblocks * 4; ++w)
-        for (int k = 0; k < 7; ++k) sum[k] += (double)hs[w * 8 + k];
-      const double nw = (double)p2.nblocks * 4, steps = sum[5];
-      printf("  stamps per wave: prologue %.0f, epilogue %.0f cycles; per step: A %.0f, B %.0f, vmcnt %.0f, barrier %.0f "
-             "(steps/wave %.1f)\n", sum[0] / nw, sum[6] / nw, sum[1] / steps, sum[2] / steps, sum[3] / steps,
-             sum[4] / steps, steps / nw);
-      unsigned long long* nul = nullptr;
-      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_x64_stamps), &nul, sizeof(nul)));
-      CK(hipFree(st));
-    }
-#endif
 #ifdef CRAM_X32_STAMPS
     {
       unsigned long long* st;
@@ -205,7 +183,7 @@ int main(int argc, char** argv) {
     const double fl = flops_of(c);
     const bool ok = nbad[1] == 0 && nnan[1] == 0 && nbad[2] == 0 && nnan[2] == 0;
     all_ok &= ok;
-    printf("%-26s lib %.3f ms (%5.0f TF/s) | x64 %.3f ms (%5.0f) x%.3f max|d| %.2e mean %.2e bad %zu nan %zu | "
+    printf("%-26s lib %.3f ms (%5.0f TF/s) | x32b %.3f ms (%5.0f) x%.3f max|d| %.2e mean %.2e bad %zu nan %zu | "
            "x32 %.3f ms (%5.0f) x%.3f max|d| %.2e mean %.2e bad %zu nan %zu %s\n",
            c.name, t[0][2], fl / t[0][2] / 1e9, t[1][2], fl / t[1][2] / 1e9, t[0][2] / t[1][2], md[1], sd[1] / no,
            nbad[1], nnan[1], t[2][2], fl / t[2][2] / 1e9, t[0][2] / t[2][2], md[2], sd[2] / no, nbad[2], nnan[2],
