@@ -164,6 +164,9 @@ def main():
     ap.add_argument("--cpu-units", type=int, default=8, help="IE units of the CPU baseline sample (>= 1)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8,
                     help="decode steps of the CPU decode baseline's sample (0 = skip it); extrapolated to --decode-tokens")
+    ap.add_argument("--cpu-decode-layers", type=int, default=-1,
+                    help="decoder layers the CPU decode sample runs, scaled to all (0 = all; -1 = 2 for prompts over "
+                         "4096 tokens, else all)")
     ap.add_argument("--decode-questions", type=int, default=0,
                     help="questions decoded once across the ranks (default: the whole 1000-question set; config 5: "
                          "one KV-budget batch per GPU)")
@@ -424,13 +427,20 @@ def main():
             log(f"[rank 0] cpu baseline {cpu['value']:.4f} heads/s on {cpu['cores']} cores")
         if want_dec:
             qc, ids, w, hd = dec_cpu_input
+            # long prompts (config 5, ~8k tokens): the hooked forward builds a dense [H, T, T] mask per hooked layer,
+            # minutes per question on the host, so the sample runs the first 2 layers and scales per layer
+            k_layers = args.cpu_decode_layers if args.cpu_decode_layers >= 0 else (2 if ids.numel() > 4096 else 0)
             r = cpu_baseline.time_decode(cpu_model, ids.cpu(), w, hd if hd else
                                          {l: list(range(H)) for l in range(L)},
-                                         new_tokens=args.decode_tokens, sampled_steps=args.cpu_decode_steps)
+                                         new_tokens=args.decode_tokens, sampled_steps=args.cpu_decode_steps,
+                                         layers=k_layers, log=log)
             cpu_dec = {"value": r["questions_per_s"], "unit": "questions/s", "cores": r["cores"], "kind": "port",
                        "method": "sampled + extrapolated",
                        "sample": (f"1 question ({dsname} #{qc}, {r['prompt_tokens']} prompt tokens, {r['heads']} "
-                                  f"hooked heads): hooks on the selected heads + greedy generate "
+                                  f"hooked heads"
+                                  + (f" in the first {r['layers_run']} of {r['layers']} layers, times scaled by "
+                                     f"{r['layers']}/{r['layers_run']}" if r["layers_run"] < r["layers"] else "")
+                                  + "): hooks on the selected heads + greedy generate "
                                   f"(re_weighting.py:115-138) of 1 + {r['sampled_steps']} tokens, {r['seconds']:.1f}s; "
                                   f"prefill {r['prefill_s']:.2f}s + {args.decode_tokens - 1} x median step "
                                   f"{r['step_s']['median']:.3f}s = {r['question_s']:.1f}s per question at "

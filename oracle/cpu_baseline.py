@@ -121,13 +121,18 @@ def sample_units(num_layers: int, num_heads: int, n: int):
 
 @torch.no_grad()
 def time_decode(model, ids: torch.Tensor, w16: torch.Tensor, layers_to_heads: dict, new_tokens: int = 100,
-                sampled_steps: int = 8) -> dict:
+                sampled_steps: int = 8, layers: int = 0, log=None) -> dict:
     """The reference's reweighted decode of one question on the CPU (re_weighting.py:115-138): forward-pre-hooks
     on the selected heads (:118-124), greedy `generate` (:127-132).  Bounded sample: generate runs 1 + sampled_steps
     tokens (min_new_tokens keeps EOS from ending it early); a StoppingCriteria stamps the clock after every token,
     so the first stamp closes the prefill (+ the first token) and the rest are the per-token decode steps.  One
     question's time at `new_tokens` = prefill + (new_tokens - 1) x median step (linear extrapolation; the per-step
-    attention cost grows by ~1 key per step, < 0.1 % of a ~900-token prompt's)."""
+    attention cost grows by ~1 key per step, < 0.1 % of a ~900-token prompt's).
+
+    layers = k > 0 (long prompts, where the hooked forward is minutes on the host: the dense [H, T, T] mask of every
+    hooked layer): the sample runs the first k decoder layers only (their weights, their hooks) and the per-layer part
+    of the time is scaled by L / k (embedding and the one-row lm_head ride along unscaled, a < 1 % under-count of the
+    reference's time)."""
     from transformers import StoppingCriteria, StoppingCriteriaList
     torch.set_num_threads(cores())
     ids = ids.reshape(1, -1).cpu()
@@ -137,9 +142,18 @@ def time_decode(model, ids: torch.Tensor, w16: torch.Tensor, layers_to_heads: di
     class _Stamp(StoppingCriteria):
         def __call__(self, input_ids, scores, **kwargs):
             stamps.append(time.perf_counter())
+            if log is not None:
+                log(f"cpu decode sample: token {len(stamps)} at {stamps[-1] - t0:.1f}s")
             return torch.zeros(input_ids.shape[0], dtype=torch.bool)
 
     n = 1 + max(1, int(sampled_steps))
+    L = model.config.num_hidden_layers
+    k = int(layers) if 0 < int(layers) < L else L
+    full_layers = model.model.layers
+    if k < L:
+        model.model.layers = full_layers[:k]
+        model.config.num_hidden_layers = k
+        layers_to_heads = {l: v for l, v in layers_to_heads.items() if int(l) < k}
     hs = hook_ref.register_hooks(model, layers_to_heads, lw)
     try:
         t0 = time.perf_counter()
@@ -148,13 +162,16 @@ def time_decode(model, ids: torch.Tensor, w16: torch.Tensor, layers_to_heads: di
     finally:
         for h in hs:
             h.remove()
+        model.model.layers = full_layers
+        model.config.num_hidden_layers = L
     if len(stamps) != n or out.shape[1] != ids.shape[1] + n:
         raise RuntimeError(f"CPU decode sample produced {out.shape[1] - ids.shape[1]} tokens, {len(stamps)} stamps")
-    prefill = stamps[0] - t0
-    steps = sorted(b - a for a, b in zip(stamps, stamps[1:]))
+    scale = L / k
+    prefill = (stamps[0] - t0) * scale
+    steps = sorted((b - a) * scale for a, b in zip(stamps, stamps[1:]))
     med = steps[len(steps) // 2]
     per_q = prefill + (max(1, int(new_tokens)) - 1) * med
     return {"prefill_s": prefill, "step_s": {"min": steps[0], "median": med, "max": steps[-1]},
             "sampled_steps": len(steps), "seconds": stamps[-1] - t0, "question_s": per_q,
             "questions_per_s": 1.0 / per_q, "cores": cores(), "prompt_tokens": int(ids.shape[1]),
-            "heads": sum(len(v) for v in layers_to_heads.values())}
+            "heads": sum(len(v) for v in layers_to_heads.values()), "layers_run": k, "layers": L}

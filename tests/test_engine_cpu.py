@@ -334,6 +334,10 @@ def test_cpu_baseline_model_matches_engine(family):
     d = cpu_baseline.time_decode(model, ids, w, {0: [1], 1: [0, 3]}, new_tokens=100, sampled_steps=3)
     assert d["sampled_steps"] == 3 and d["prefill_s"] > 0 and d["heads"] == 3
     assert d["question_s"] == pytest.approx(d["prefill_s"] + 99 * d["step_s"]["median"])
+    # the long-prompt form: the first layer only, times scaled by L / k; the model is whole again afterwards
+    d1 = cpu_baseline.time_decode(model, ids, w, {0: [1], 1: [0, 3]}, new_tokens=100, sampled_steps=2, layers=1)
+    assert (d1["layers_run"], d1["layers"], d1["heads"]) == (1, 2, 1)
+    assert len(model.model.layers) == 2 and model.config.num_hidden_layers == 2
     # the hooked greedy ids of the sample equal the engine's batched decode with the same bias
     hs = hook_ref.register_hooks(model, {0: [1], 1: [0, 3]}, hook_ref.log_weight(w))
     try:
