@@ -67,9 +67,20 @@ __device__ __forceinline__ f32x4 mfma16(const u32x4& a, const u32x4& b, const f3
                                                 0);
 }
 
-// round to the element type and back (the model-dtype rounding transformers applies between ops)
-template <typename T>
-__device__ __forceinline__ float rnd(float x) { return (float)(T)x; }
+// round to the element type and back (the model-dtype rounding transformers applies between ops).  Not as
+// (float)(T)x: the compiler folds that pair away in some contexts (cram_fused.hip measured 1-ulp RoPE mismatches on
+// ROCm 7.2, and so did the RoPE epilogue here), so bf16 rounds by integer RNE and fp16's hardware conversion is
+// pinned in a register.  Inputs are finite.
+template <typename T> __device__ __forceinline__ float rnd(float x);
+template <> __device__ __forceinline__ float rnd<__bf16>(float x) {
+  const unsigned u = __float_as_uint(x);
+  return __uint_as_float((u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u);
+}
+template <> __device__ __forceinline__ float rnd<_Float16>(float x) {
+  unsigned short b = __builtin_bit_cast(unsigned short, (_Float16)x);
+  asm volatile("" : "+v"(b));
+  return (float)__builtin_bit_cast(_Float16, b);
+}
 
 constexpr int BM = 256;            // activation rows per tile (y)
 constexpr int BN = 256;            // weight rows per tile (x)
@@ -81,11 +92,21 @@ constexpr int LDS_BYTES = 2 * STAGE;
 
 // internal epilogue of the split-K form: fp32 partial sums of one K range, combined by gemm_combine_kernel
 constexpr int EPI_PARTIAL = 100;
+// internal epilogue of cram_gemm_residual: out = rnd(res + rnd(acc)), the decoder layer's residual add
+constexpr int EPI_RESIDUAL = 101;
+// internal epilogue of cram_gemm_rope (4-wave kernel only): the q | k | v projection with cram_rope_split's RoPE
+constexpr int EPI_ROPE = 102;
 
 struct GemmParams {
   const void* x; int64_t ldx;      // weights [N, K]
   const void* y; int64_t ldy;      // activations [M, K]
   void* out; int64_t ldo;          // [M, N] (store) or [M, N / 2] (silu-mul); EPI_PARTIAL: fp32 [splits][M][N]
+  const void* res; int64_t ldr;    // EPI_RESIDUAL: the residual stream [M, N] (may be out itself)
+  // EPI_ROPE (head dim 128; a wave's 128 output columns are one head): see cram_gemm_rope in cram_attn.h
+  const void* cos_t; const void* sin_t; int64_t tab_rs;
+  const int64_t* pos; const int64_t* dst_b;
+  void* kout; void* vout; int64_t kv_bs, kv_hs, kv_rs;
+  int rows, T, hq, hkv, kv_row0, keep_k;
   int M, N, K;
   int ntm, ntn, nblocks;
   int splits, kts;                 // split-K: K ranges per output tile, K-tiles per range (K = splits * kts * BK)
@@ -129,6 +150,12 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[NA][NB], const Gem
           V4 v;
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = (T)acc[a][b][i];
+          *reinterpret_cast<V4*>(ob + (int64_t)mb * p.ldo + n + 16 * a) = v;
+        } else if constexpr (EPI == EPI_RESIDUAL) {
+          const V4 r = *reinterpret_cast<const V4*>(static_cast<const T*>(p.res) + (int64_t)mb * p.ldr + n + 16 * a);
+          V4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (T)((float)r[i] + rnd<T>(acc[a][b][i]));
           *reinterpret_cast<V4*>(ob + (int64_t)mb * p.ldo + n + 16 * a) = v;
         } else if ((a & 2) == 0) {
           // gate tiles a = 0, 1 (mod 4) and their up tiles a + 2 (weight rows interleaved in blocks of 32): the gate
@@ -486,18 +513,69 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   // 8-byte stores per lane -- the 8-byte form left each workgroup a long store-issue tail).  Lane (r, g) holds acc tile
   // (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]; each wave rounds its 128 rows (256 B each, or 128 B of SiLU-mul
   // output) into its own 32 KiB of the (now idle) ring, 8-byte units swizzled by row so a ds_write lane group spreads
-  // over the banks, then reads back whole 16-byte row pieces and stores them.
-  __syncthreads();                               // every wave's last fragment reads are done (no LDS-DMA is pending)
+  // over the banks, then reads back whole 16-byte row pieces and stores them (EPI_RESIDUAL: plus the residual piece
+  // at the same place, all 32 fetched before the staging so their latency hides behind it).
   using V4 = typename GVec<T>::x4;
   using V8 = typename GVec<T>::x8;
-  constexpr int RB = EPI == CRAM_GEMM_STORE ? 256 : 128;      // staged bytes per row
+  constexpr bool ROWS = EPI != CRAM_GEMM_SILU_MUL;            // one staged row = 128 output columns
+  constexpr int RB = ROWS ? 256 : 128;                         // staged bytes per row
+  constexpr int LPR = RB / 16;                                 // read-back lanes per row: 16 | 8
+  constexpr int RPI = 64 / LPR;                                // rows per read-back instruction: 4 | 8
+  constexpr int NRB = 128 / RPI;                               // read-back instructions per wave
+  const int cl = lane % LPR, rl = lane / LPR;
+  const int64_t col0 = ROWS ? (int64_t)n0 + 128 * wn + 8 * cl : (int64_t)(n0 / 2) + 64 * wn + 8 * cl;
+  const int mw = m0 + 128 * wm;                                // the wave's first output row
+  // EPI_ROPE: the wave's head (wave-uniform) -- q heads rotate into out, k heads into kout, v heads are copied into
+  // vout (with keep_k the k and v heads also stay in out); without kout every head goes to out (q, k rotated)
+  const int hidx = (n0 + 128 * wn) >> 7;
+  const int kind = EPI != EPI_ROPE ? 0 : (hidx < p.hq ? 0 : (hidx < p.hq + p.hkv ? 1 : 2));
+  const bool rot = EPI == EPI_ROPE && kind < 2;
+  V8 rv[EPI == EPI_RESIDUAL ? NRB : 1];
+  if constexpr (EPI == EPI_RESIDUAL) {
+    const T* rb = static_cast<const T*>(p.res);
+#pragma unroll
+    for (int j = 0; j < NRB; ++j) {
+      const int m = mw + RPI * j + rl;
+      if (m < p.M) rv[j] = *reinterpret_cast<const V8*>(rb + (int64_t)m * p.ldr + col0);
+    }
+  }
+  __syncthreads();                               // every wave's last fragment reads are done (no LDS-DMA is pending)
   char* const wl = smem + wave * 32768;
   auto swz = [](int row) { return RB == 256 ? (row & 7) << 2 : ((row >> 1) & 3) << 2; };   // unit XOR (bits 2..4)
   static_for<8>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
     const int ml = 16 * b + fr;                  // the lane's row within the wave's 128
     const int sw = swz(ml);
-    if constexpr (EPI == CRAM_GEMM_STORE) {
+    bool staged = false;
+    if constexpr (EPI == EPI_ROPE) {
+      if (rot) {
+        // rotation pairs (c, c + 64) of the wave's head sit in the same lane: tiles a and a + 4, element i.
+        // rope_kernel's arithmetic on the rounded projection: x1' = rnd(rnd(x1 c1) + rnd(-x2 s1)),
+        // x2' = rnd(rnd(x2 c2) + rnd(x1 s2)), table row = pos[m] (or m % T)
+        const int m = mw + ml;
+        const int64_t pp = m < p.rows ? (p.pos ? p.pos[m] : (int64_t)(m % p.T)) : 0;
+        const T* ct = static_cast<const T*>(p.cos_t) + pp * p.tab_rs + 4 * fg;
+        const T* st = static_cast<const T*>(p.sin_t) + pp * p.tab_rs + 4 * fg;
+        static_for<4>([&](auto ai) {
+          constexpr int a = decltype(ai)::value;
+          const V4 c1 = *reinterpret_cast<const V4*>(ct + 16 * a), c2 = *reinterpret_cast<const V4*>(ct + 64 + 16 * a);
+          const V4 s1 = *reinterpret_cast<const V4*>(st + 16 * a), s2 = *reinterpret_cast<const V4*>(st + 64 + 16 * a);
+          const f32x4 v1 = acc4<4 * (8 * a + b)>(), v2 = acc4<4 * (8 * (a + 4) + b)>();
+          V4 o1, o2;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float x1 = rnd<T>(v1[i]), x2 = rnd<T>(v2[i]);
+            o1[i] = (T)(rnd<T>(x1 * (float)c1[i]) + rnd<T>(-x2 * (float)s1[i]));
+            o2[i] = (T)(rnd<T>(x2 * (float)c2[i]) + rnd<T>(x1 * (float)s2[i]));
+          }
+          *reinterpret_cast<V4*>(wl + ml * RB + (((4 * a + fg) ^ sw) * 8)) = o1;
+          *reinterpret_cast<V4*>(wl + ml * RB + (((4 * (a + 4) + fg) ^ sw) * 8)) = o2;
+        });
+        staged = true;
+      }
+    }
+    if (staged) {
+    } else if constexpr (ROWS) {
       static_for<8>([&](auto ai) {
         constexpr int a = decltype(ai)::value;
         const f32x4 v = acc4<4 * (8 * a + b)>();
@@ -524,17 +602,40 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
     }
   });
   // each wave reads back only its own rows: its writes are ordered before its reads (no barrier needed)
-  constexpr int LPR = RB / 16;                   // lanes per row: 16 | 8
-  constexpr int RPI = 64 / LPR;                  // rows per instruction: 4 | 8
-  const int cl = lane % LPR, rl = lane / LPR;
   T* ob = static_cast<T*>(p.out);
-  const int64_t col0 = EPI == CRAM_GEMM_STORE ? (int64_t)n0 + 128 * wn + 8 * cl : (int64_t)(n0 / 2) + 64 * wn + 8 * cl;
+  if constexpr (EPI == EPI_RESIDUAL) {
+#pragma unroll
+    for (int j = 0; j < NRB; ++j) {              // fully unrolled: rv stays in registers
+      const int ml = RPI * j + rl;
+      V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (T)((float)rv[j][i] + (float)v[i]);
+      if (mw + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mw + ml) * p.ldo + col0) = v;
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    const bool split = p.kout != nullptr;
+    const bool to_out = !split || kind == 0 || p.keep_k;        // keep_k: the k / v heads stay in out too
+    T* const kvb = static_cast<T*>(kind == 2 ? p.vout : p.kout) +
+                   (int64_t)(hidx - p.hq - (kind == 2 ? p.hkv : 0)) * p.kv_hs + 8 * cl;
 #pragma unroll 4
-  for (int j = 0; j < 128 / RPI; ++j) {
-    const int ml = RPI * j + rl;
-    const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
-    const int m = m0 + 128 * wm + ml;
-    if (m < p.M) *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + col0) = v;
+    for (int j = 0; j < NRB; ++j) {
+      const int ml = RPI * j + rl;
+      const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
+      const int m = mw + ml;
+      if (to_out && m < p.M) *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + col0) = v;
+      if (split && kind != 0 && m < p.rows) {
+        const int64_t sb = p.dst_b ? p.dst_b[m] : (int64_t)(m / p.T);
+        const int64_t t = p.dst_b ? p.pos[m] : (int64_t)(m % p.T);
+        *reinterpret_cast<V8*>(kvb + sb * p.kv_bs + (p.kv_row0 + t) * p.kv_rs) = v;
+      }
+    }
+  } else {
+#pragma unroll 4
+    for (int j = 0; j < NRB; ++j) {
+      const int ml = RPI * j + rl;
+      const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
+      if (mw + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mw + ml) * p.ldo + col0) = v;
+    }
   }
 }
 
@@ -592,48 +693,105 @@ inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 1
 
 }  // namespace
 
-extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N,
-                         int K, int epilogue, int dtype, cram_stream_t stream) {
-  if (!y || !x || !out || M <= 0 || N <= 0 || K <= 0) return CRAM_ERR_INVALID_ARG;
-  if (epilogue != CRAM_GEMM_STORE && epilogue != CRAM_GEMM_SILU_MUL) return CRAM_ERR_INVALID_ARG;
+namespace {
+
+// shared by cram_gemm and cram_gemm_residual: argument checks, then the 4-wave kernel (bf16, >= 2 K-tiles, 16-byte
+// output rows) or the 8-wave one
+int gemm_launch(GemmParams& p, int epi, int dtype, hipStream_t st) {
+  if (!p.y || !p.x || !p.out || p.M <= 0 || p.N <= 0 || p.K <= 0) return CRAM_ERR_INVALID_ARG;
   if (dtype != CRAM_DTYPE_BF16 && dtype != CRAM_DTYPE_F16) return CRAM_ERR_UNSUPPORTED;
-  if (N % BN != 0 || K % BK != 0) return CRAM_ERR_UNSUPPORTED;
-  if (!al16(y) || !al16(x) || !al16(out) || (ldy & 7) || (ldx & 7) || (ldo & 3)) return CRAM_ERR_ALIGNMENT;
-  const int nout = epilogue == CRAM_GEMM_STORE ? N : N / 2;
-  if (ldy < K || ldx < K || ldo < nout) return CRAM_ERR_INVALID_ARG;
+  if (p.N % BN != 0 || p.K % BK != 0) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(p.y) || !al16(p.x) || !al16(p.out) || (p.ldy & 7) || (p.ldx & 7) || (p.ldo & 3)) return CRAM_ERR_ALIGNMENT;
+  const int nout = epi == CRAM_GEMM_SILU_MUL ? p.N / 2 : p.N;
+  if (p.ldy < p.K || p.ldx < p.K || p.ldo < nout) return CRAM_ERR_INVALID_ARG;
   // buffer-descriptor extents (one 256-row tile) are 32-bit byte counts
-  if ((int64_t)BN * ldx * 2 >= (1ll << 31) || (int64_t)BM * ldy * 2 >= (1ll << 31)) return CRAM_ERR_UNSUPPORTED;
-  GemmParams p;
-  p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo;
-  p.M = M; p.N = N; p.K = K;
-  p.splits = 1; p.kts = K / BK;
-  p.ntm = (M + BM - 1) / BM;
-  p.ntn = N / BN;
+  if ((int64_t)BN * p.ldx * 2 >= (1ll << 31) || (int64_t)BM * p.ldy * 2 >= (1ll << 31)) return CRAM_ERR_UNSUPPORTED;
+  p.splits = 1; p.kts = p.K / BK;
+  p.ntm = (p.M + BM - 1) / BM;
+  p.ntn = p.N / BN;
   const int64_t nb = (int64_t)p.ntm * p.ntn;
   if (nb > 0x7fffffff) return CRAM_ERR_INVALID_ARG;
   p.nblocks = (int)nb;
-  const hipStream_t st = (hipStream_t)stream;
   const dim3 g(p.nblocks);
   int kv = -1;
   cram_get_knob(CRAM_KNOB_GEMM_VARIANT, &kv);
   // tile order of the 4-wave kernel: groups of 8 activation tiles for short, narrow GEMMs (q/k/v, o_proj: N <= 6144,
   // K <= 4096: 1.02-1.03x the other order), groups of 8 weight tiles otherwise (down_proj: 1.07x; gate/up: equal)
   // (tools/gemm_ab_knob.py, r04); knob 2 forces the activation-tile groups, 1 the weight-tile groups (A/B)
-  p.raster = kv == 2 ? 2 : (kv == 1 ? 0 : ((N <= 6144 && K <= 4096) ? 2 : 0));
-  if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && (ldo & 7) == 0 && kv != 0) {   // (16-byte output rows)
-    if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE>), g, dim3(256), 0, st, p);
+  p.raster = kv == 2 ? 2 : (kv == 1 ? 0 : ((p.N <= 6144 && p.K <= 4096) ? 2 : 0));
+  if (epi == EPI_ROPE) {                         // the 4-wave kernel only (the C-ABI checked bf16, kts >= 2)
+    hipLaunchKernelGGL((gemm_w4_kernel<__bf16, EPI_ROPE>), g, dim3(256), 0, st, p);
+    return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+  }
+  if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && (p.ldo & 7) == 0 && kv != 0) {   // (16-byte output rows)
+    if (epi == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE>), g, dim3(256), 0, st, p);
+    else if (epi == EPI_RESIDUAL) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, EPI_RESIDUAL>), g, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL>), g, dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
   }
   const dim3 blk(512);
   if (dtype == CRAM_DTYPE_BF16) {
-    if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<__bf16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
+    if (epi == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<__bf16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
+    else if (epi == EPI_RESIDUAL) hipLaunchKernelGGL((gemm_tn_kernel<__bf16, EPI_RESIDUAL>), g, blk, 0, st, p);
     else hipLaunchKernelGGL((gemm_tn_kernel<__bf16, CRAM_GEMM_SILU_MUL>), g, blk, 0, st, p);
   } else {
-    if (epilogue == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
+    if (epi == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_STORE>), g, blk, 0, st, p);
+    else if (epi == EPI_RESIDUAL) hipLaunchKernelGGL((gemm_tn_kernel<_Float16, EPI_RESIDUAL>), g, blk, 0, st, p);
     else hipLaunchKernelGGL((gemm_tn_kernel<_Float16, CRAM_GEMM_SILU_MUL>), g, blk, 0, st, p);
   }
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}
+
+}  // namespace
+
+extern "C" int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N,
+                         int K, int epilogue, int dtype, cram_stream_t stream) {
+  if (epilogue != CRAM_GEMM_STORE && epilogue != CRAM_GEMM_SILU_MUL) return CRAM_ERR_INVALID_ARG;
+  GemmParams p{};
+  p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo;
+  p.M = M; p.N = N; p.K = K;
+  return gemm_launch(p, epilogue, dtype, (hipStream_t)stream);
+}
+
+extern "C" int cram_gemm_residual(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* res,
+                                  int64_t ldr, void* out, int64_t ldo, int M, int N, int K, int dtype,
+                                  cram_stream_t stream) {
+  if (!res || M <= 0 || N <= 0) return CRAM_ERR_INVALID_ARG;
+  if (!al16(res) || (ldr & 7) || (ldo & 7)) return CRAM_ERR_ALIGNMENT;
+  if (ldr < N) return CRAM_ERR_INVALID_ARG;
+  // the residual may be the output itself (every element is read, then written, by the same lane); any other overlap
+  // of the two [M][N] spans is rejected
+  const char* r0 = static_cast<const char*>(res);
+  const char* o0 = static_cast<const char*>(out);
+  if (r0 != o0 || ldr != ldo) {
+    const int64_t rspan = ((int64_t)(M - 1) * ldr + N) * 2, ospan = ((int64_t)(M - 1) * ldo + N) * 2;
+    if (r0 < o0 + ospan && o0 < r0 + rspan) return CRAM_ERR_INVALID_ARG;
+  }
+  GemmParams p{};
+  p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo; p.res = res; p.ldr = ldr;
+  p.M = M; p.N = N; p.K = K;
+  return gemm_launch(p, EPI_RESIDUAL, dtype, (hipStream_t)stream);
+}
+
+extern "C" int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M,
+                              int K, int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t,
+                              int64_t tab_rs, const int64_t* pos, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs,
+                              int64_t kv_rs, int kv_row0, const int64_t* dst_b, int keep_k, int dtype,
+                              cram_stream_t stream) {
+  if (!cos_t || !sin_t || rows < 0 || rows > M || T <= 0 || hq <= 0 || hkv <= 0 || kv_row0 < 0)
+    return CRAM_ERR_INVALID_ARG;
+  if ((kout == nullptr) != (vout == nullptr) || (dst_b && !pos) || (kout && !dst_b && rows % T != 0))
+    return CRAM_ERR_INVALID_ARG;
+  if (dtype != CRAM_DTYPE_BF16 || d != 128 || K % BK != 0 || K / BK < 2) return CRAM_ERR_UNSUPPORTED;
+  if ((ldo & 7) || (tab_rs & 7) || !al16(cos_t) || !al16(sin_t)) return CRAM_ERR_ALIGNMENT;
+  if (kout && ((kv_bs & 7) || (kv_hs & 7) || (kv_rs & 7) || !al16(kout) || !al16(vout))) return CRAM_ERR_ALIGNMENT;
+  GemmParams p{};
+  p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo;
+  p.M = M; p.N = (hq + 2 * hkv) * d; p.K = K;
+  p.cos_t = cos_t; p.sin_t = sin_t; p.tab_rs = tab_rs; p.pos = pos; p.dst_b = dst_b;
+  p.kout = kout; p.vout = vout; p.kv_bs = kv_bs; p.kv_hs = kv_hs; p.kv_rs = kv_rs;
+  p.rows = rows; p.T = T; p.hq = hq; p.hkv = hkv; p.kv_row0 = kv_row0; p.keep_k = keep_k;
+  return gemm_launch(p, EPI_ROPE, dtype, (hipStream_t)stream);
 }
 
 extern "C" size_t cram_gemm_splitk_workspace_size(int M, int N, int splits) {

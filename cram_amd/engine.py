@@ -82,6 +82,12 @@ class ModelSpec:
 ROW_ALIGN = 256
 # gate/up + SiLU-mul on cram_gemm's fused epilogue (CrAMEngine.mlp); CRAM_FUSED_MLP=0: hipBLASLt + cram_silu_mul (A/B)
 FUSED_MLP = os.environ.get("CRAM_FUSED_MLP", "1") != "0"
+# o_proj / down_proj with the residual add in cram_gemm's epilogue (CrAMEngine.o_proj_norm / mlp_residual) at the same
+# row counts; CRAM_FUSED_RESIDUAL=0: the add inside the next RMSNorm instead (A/B)
+FUSED_RESIDUAL = os.environ.get("CRAM_FUSED_RESIDUAL", "1") != "0"
+# q/k/v projection with RoPE in cram_gemm's epilogue (bf16, head_dim 128, no q/k/v bias) at the same row counts;
+# CRAM_FUSED_QKV=0: hipBLASLt + cram_rope_inplace / cram_rope_split (A/B)
+FUSED_QKV = os.environ.get("CRAM_FUSED_QKV", "1") != "0"
 # packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where hipBLASLt already runs at full rate
 PREFILL_CHUNK_ROWS = 32768
 
@@ -238,6 +244,24 @@ class CrAMEngine:
             act = ops.silu_mul(ops.linear(x, lw.wgu), F)
         return ops.linear(act, lw.wd)
 
+    def o_proj_norm(self, a: torch.Tensor, lw: LayerW, h: torch.Tensor):
+        """(h + o_proj(a), RMSNorm_ln2 of it) over row buffers a [M, q_size], h [M, D].  At the fused kernels' row
+        counts the residual add runs in o_proj's epilogue (cram_gemm_residual) and the norm reads one tensor;
+        otherwise o_proj is F.linear and the add runs inside the norm.  Same rounding points either way."""
+        if self._fused_residual_ok(a):
+            h2 = ops.gemm(a, lw.wo, residual=h)
+            return h2, ops.rmsnorm(h2, lw.ln2, self.spec.eps)
+        return ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, self.spec.eps, residual=h)
+
+    def mlp_residual(self, x: torch.Tensor, lw: LayerW, h: torch.Tensor):
+        """The MLP half of a decoder layer over row buffers x, h [M, D]: (h + mlp(x), None) with the add in
+        down_proj's epilogue at the fused kernels' row counts, else (h, mlp(x)) -- the add left pending for the next
+        consumer's RMSNorm (its residual input)."""
+        if self._fused_residual_ok(x):
+            act = ops.gemm(x, self._gate_up_interleaved(lw), ops.GEMM_SILU_MUL)
+            return ops.gemm(act, lw.wd, residual=h), None
+        return h, self.mlp(x, lw)
+
     # gate/up with the fused activation: bf16 (the 4-wave kernel's type), 256-row tiles filled, the weight interleaved
     FUSED_MLP_MIN_ROWS = 4096
 
@@ -247,6 +271,16 @@ class CrAMEngine:
         D, F = self.spec.hidden, self.spec.intermediate
         M = x.numel() // x.shape[-1]
         return M >= self.FUSED_MLP_MIN_ROWS and (2 * F) % 256 == 0 and D % 64 == 0 and D >= 128
+
+    def _fused_qkv_ok(self, x: torch.Tensor, lw: LayerW) -> bool:
+        sp = self.spec
+        return (FUSED_QKV and lw.bqkv is None and self._fused_mlp_ok(x) and sp.head_dim == 128
+                and (sp.num_heads + 2 * sp.num_kv_heads) % 2 == 0)
+
+    def _fused_residual_ok(self, x: torch.Tensor) -> bool:
+        sp = self.spec
+        return (FUSED_RESIDUAL and self._fused_mlp_ok(x) and sp.hidden % 256 == 0 and sp.q_size % 64 == 0
+                and sp.intermediate % 64 == 0)
 
     def _gate_up_interleaved(self, lw: LayerW) -> torch.Tensor:
         """lw.wgu with gate / up rows interleaved in blocks of 32 (cram_gemm's SiLU-mul layout), rebuilt whenever the
@@ -294,7 +328,8 @@ class CrAMEngine:
         alignment padding (GEMM M from padded_rows: the 256-row macro tile, then the measured row table; padding rows carry
         garbage and are never read back).  The layer input is hbuf [Mp, D], or hbuf + delta when the previous
         layer's MLP output is still pending (the residual add then runs inside this layer's first RMSNorm).
-        Returns (h, mlp_out): the layer output is h + mlp_out, left for the next consumer to fuse.
+        Returns (h, mlp_out): the layer output is h + mlp_out, left for the next consumer to fuse (mlp_out None: h
+        is the layer output, the add ran in down_proj's epilogue).
         out_rows=n returns [B*n, D] pairs (last n rows of every sequence).
 
         prefix=(k0, v0, pos): the B sequences are SUFFIXES that start at position p0 = k0.shape[1] of a common
@@ -306,12 +341,14 @@ class CrAMEngine:
             x = ops.rmsnorm(hbuf, lw.ln1, sp.eps)
         else:
             hbuf, x = ops.rmsnorm(delta, lw.ln1, sp.eps, residual=hbuf)
-        y = ops.linear(x, lw.wqkv, lw.bqkv)
-        yr = y[:M]
-        y3 = yr.view(B, T, -1)
-        q = y3[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
+        fused = self._fused_qkv_ok(x, lw)            # RoPE in the q/k/v GEMM's epilogue (cram_gemm_rope)
         if prefix is None:
-            ops.rope_inplace(yr, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
+            if fused:
+                y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M)
+            else:
+                y = ops.linear(x, lw.wqkv, lw.bqkv)
+                ops.rope_inplace(y[:M], sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
+            y3 = y[:M].view(B, T, -1)
             k = y3[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
             v = y3[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
         else:                                        # [prefix | suffix] keys per sequence
@@ -322,7 +359,14 @@ class CrAMEngine:
             k[:, :p0] = k0
             v[:, :p0] = v0
             # q roped in place; the suffix's roped k and its v land behind the prefix (no copy pass)
-            ops.rope_split(yr, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)
+            if fused:
+                y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M,
+                                  kout=k, vout=v, row0=p0, pos=pos)
+            else:
+                y = ops.linear(x, lw.wqkv, lw.bqkv)
+                ops.rope_split(y[:M], sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)
+            y3 = y[:M].view(B, T, -1)
+        q = y3[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
         if out_rows is None:
             a = torch.empty((hbuf.shape[0], sp.q_size), dtype=self.dtype, device=self.device)
             ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale, bias=bias,
@@ -334,8 +378,8 @@ class CrAMEngine:
             ops.attn_prefill(q[:, -n:].transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale,
                              bias=bias, enable=enable, W=W, out=a.view(B, n, sp.num_heads, sp.head_dim))
             hres = hbuf[:M].view(B, T, -1)[:, -n:].reshape(B * n, -1)
-        h2, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=hres)
-        return h2, self.mlp(x2, lw)
+        h2, x2 = self.o_proj_norm(a, lw, hres)
+        return self.mlp_residual(x2, lw, h2)
 
     @torch.no_grad()
     def forward_hidden(self, ids: torch.Tensor, cb: Optional[CredibilityBias] = None,
@@ -580,13 +624,17 @@ class DecodeSession:
                 x = ops.rmsnorm(h, lw.ln1, sp.eps)
             else:
                 h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
-            y = ops.linear(x, lw.wqkv, lw.bqkv)
-            yr = y[:total]
             # q and k roped in place (the varlen attention reads them there), roped k and v also written straight
             # into the cache rows (sequence bidx, position pos) of this layer
-            ops.rope_split(yr, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
-                           self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2), 0, pos=pos, dst_b=bidx,
-                           keep_k=True)
+            kc, vc = self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2)
+            if eng._fused_qkv_ok(x, lw):
+                y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
+                                  rows=total, kout=kc, vout=vc, row0=0, pos=pos, dst_b=bidx, keep_k=True)
+            else:
+                y = ops.linear(x, lw.wqkv, lw.bqkv)
+                ops.rope_split(y[:total], sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1, kc, vc,
+                               0, pos=pos, dst_b=bidx, keep_k=True)
+            yr = y[:total]
             q = yr[:, :sp.q_size].view(total, sp.num_heads, sp.head_dim)
             if l == sp.num_layers - 1:
                 # last layer: every row's K/V is in the cache now and only the last rows feed the logits, so their
@@ -606,9 +654,9 @@ class DecodeSession:
             ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=bias,
                                     enable=self.cb.enable[l, b0:b1], W=self.cb.W,
                                     out=a[:total].view(total, sp.num_heads, sp.head_dim))
-            h, x2 = ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, sp.eps, residual=h)
-            m = eng.mlp(x2, lw)
-        _, hn = ops.rmsnorm(m, eng.norm, sp.eps, residual=h)
+            h, x2 = eng.o_proj_norm(a, lw, h)
+            h, m = eng.mlp_residual(x2, lw, h)
+        hn = ops.rmsnorm(h, eng.norm, sp.eps) if m is None else ops.rmsnorm(m, eng.norm, sp.eps, residual=h)[1]
         self.tokens[b0:b1] = self._pick(ops.linear(hn, eng.lm_head), slice(b0, b1))
 
     def _step_body(self):

@@ -377,9 +377,10 @@ def interleave_gate_up(wgu: torch.Tensor, F: int) -> torch.Tensor:
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, epilogue: int = GEMM_STORE, out: Optional[torch.Tensor] = None,
-         name: str = "cram_gemm") -> torch.Tensor:
+         name: str = "cram_gemm", residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x [..., K] @ w[N, K]^T on the hand-written MFMA GEMM (cram_gemm); GEMM_SILU_MUL takes an interleaved gate/up
-    weight (interleave_gate_up) and returns the MLP activation [..., N/2]."""
+    weight (interleave_gate_up) and returns the MLP activation [..., N/2].  residual [..., N] (GEMM_STORE only):
+    returns residual + x @ w^T with the add in the epilogue (cram_gemm_residual; `out` may be residual itself)."""
     _dt(x)
     if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
         raise ValueError("w must be a [N, K] row-major weight of x's dtype")
@@ -392,10 +393,77 @@ def gemm(x: torch.Tensor, w: torch.Tensor, epilogue: int = GEMM_STORE, out: Opti
     if out is None:
         out = torch.empty(x.shape[:-1] + (nout,), dtype=x.dtype, device=x.device)
     o2 = _rows2d(out, "out")
-    ev = TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout), x.device) if TIMER.enabled else None
-    code = _lib.load().cram_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(), o2.stride(0),
-                                 M, N, K, int(epilogue), _dt(x), _stream(x.device))
-    _lib.check(code, "cram_gemm")
+    if residual is not None:
+        if epilogue != GEMM_STORE or residual.dtype != x.dtype or residual.shape[-1] != N:
+            raise ValueError("residual must be a [..., N] tensor of x's dtype (GEMM_STORE only)")
+        r2 = _rows2d(residual, "residual")
+        if r2.shape[0] != M:
+            raise ValueError(f"residual has {r2.shape[0]} rows, x has {M}")
+    rbytes = 0 if residual is None else 2.0 * M * N
+    ev = (TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout) + rbytes, x.device)
+          if TIMER.enabled else None)
+    if residual is None:
+        code = _lib.load().cram_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
+                                     o2.stride(0), M, N, K, int(epilogue), _dt(x), _stream(x.device))
+        _lib.check(code, "cram_gemm")
+    else:
+        code = _lib.load().cram_gemm_residual(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), r2.data_ptr(),
+                                              r2.stride(0), o2.data_ptr(), o2.stride(0), M, N, K, _dt(x),
+                                              _stream(x.device))
+        _lib.check(code, "cram_gemm_residual")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(x.device))
+    return out
+
+
+def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int, cos: torch.Tensor,
+              sin: torch.Tensor, T: int, rows: Optional[int] = None, kout: Optional[torch.Tensor] = None,
+              vout: Optional[torch.Tensor] = None, row0: int = 0, pos: Optional[torch.Tensor] = None,
+              dst_b: Optional[torch.Tensor] = None, keep_k: bool = False, out: Optional[torch.Tensor] = None,
+              name: str = "cram_gemm") -> torch.Tensor:
+    """The q | k | v projection x @ w^T with RoPE in the GEMM epilogue (cram_gemm_rope, the 4-wave kernel; bf16,
+    head_dim 128, no bias).  Without kout / vout: ``rope_inplace`` over the q and k heads of the result (T, pos as
+    there).  With them: ``rope_split`` into kout / vout ([B, S, hkv, d] views, row0, pos, dst_b, keep_k as there),
+    for the first ``rows`` rows of x (default all; rows beyond are GEMM padding).  Returns the [M, N] buffer: q
+    rotated; k rotated and v as computed unless kout is given without keep_k (then those columns are not written)."""
+    _dt(x)
+    if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("w must be a [N, K] row-major weight of x's dtype")
+    x2 = _rows2d(x, "x")
+    M, K = x2.shape
+    N = w.shape[0]
+    if w.shape[1] != K or N != (hq + 2 * hkv) * head_dim:
+        raise ValueError(f"w must be [(hq + 2 hkv) * head_dim, K], got {tuple(w.shape)}")
+    rows = M if rows is None else int(rows)
+    if cos.dtype != x.dtype or sin.dtype != x.dtype or cos.shape != sin.shape or cos.stride(-1) != 1:
+        raise ValueError("cos/sin must be [P, d] tables of x's dtype")
+    if pos is not None and (pos.dtype != torch.int64 or pos.numel() < rows or pos.device != x.device):
+        raise ValueError("pos must be a device int64 tensor with one entry per row")
+    if (kout is None) != (vout is None):
+        raise ValueError("kout and vout go together")
+    if kout is not None:
+        for t in (kout, vout):
+            if (t.dtype != x.dtype or t.device != x.device or t.dim() != 4 or tuple(t.shape[2:]) != (hkv, head_dim)
+                    or t.stride(3) != 1):
+                raise ValueError("kout/vout must be [B, S, hkv, head_dim] views with a contiguous last dimension")
+        if kout.stride()[:3] != vout.stride()[:3]:
+            raise ValueError("kout and vout must share their strides")
+        if dst_b is None and (rows % T or rows // T > kout.shape[0] or row0 + T > kout.shape[1]):
+            raise ValueError("kout/vout must hold rows / T sequences of at least row0 + T rows")
+        if dst_b is not None and (pos is None or dst_b.dtype != torch.int64 or dst_b.numel() < rows
+                                  or dst_b.device != x.device):
+            raise ValueError("dst_b needs pos and must be a device int64 tensor with one entry per row")
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (N,), dtype=x.dtype, device=x.device)
+    o2 = _rows2d(out, "out")
+    ev = TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), x.device) if TIMER.enabled else None
+    st = (0, 0, 0) if kout is None else (kout.stride(0), kout.stride(2), kout.stride(1))
+    code = _lib.load().cram_gemm_rope(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
+                                      o2.stride(0), M, K, rows, int(T), int(hq), int(hkv), int(head_dim),
+                                      cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), _ptr(kout),
+                                      _ptr(vout), st[0], st[1], st[2], int(row0), _ptr(dst_b), int(bool(keep_k)),
+                                      _dt(x), _stream(x.device))
+    _lib.check(code, "cram_gemm_rope")
     if ev is not None:
         ev.record(torch.cuda.current_stream(x.device))
     return out

@@ -114,8 +114,8 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     lw = eng.layers[l]
     hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
     hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
-    h, x2 = ops.rmsnorm(ops.linear(abuf, lw.wo), lw.ln2, sp.eps, residual=hin)   # [Mp, D]
-    m = eng.mlp(x2, lw)                                                 # layer output h + m, add deferred
+    h, x2 = eng.o_proj_norm(abuf, lw, hin)                             # [Mp, D]
+    h, m = eng.mlp_residual(x2, lw, h)                                  # layer output h (+ m when deferred)
     if not last:
         cos, sin = eng.rope_tables(T_full)
         pos = None
@@ -126,7 +126,10 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
             h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m,
                                   prefix=pre)
     rows = Hv * n_ans
-    _, y = ops.rmsnorm(m[:rows], eng.norm, sp.eps, residual=h[:rows])   # final norm of h + m
+    if m is None:
+        y = ops.rmsnorm(h[:rows], eng.norm, sp.eps)
+    else:
+        _, y = ops.rmsnorm(m[:rows], eng.norm, sp.eps, residual=h[:rows])   # final norm of h + m
     return y.view(Hv, n_ans, sp.hidden)                                 # [Hv, n, D]
 
 

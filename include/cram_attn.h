@@ -48,8 +48,9 @@ extern "C" {
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
 
-#define CRAM_ABI_VERSION 4        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
-                                     4: cram_get_knob(which, *value), decode projection GEMM */
+#define CRAM_ABI_VERSION 5        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
+                                     4: cram_get_knob(which, *value), decode projection GEMM;
+                                     5: cram_gemm_residual, cram_gemm_rope */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -198,6 +199,32 @@ int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows
 #define CRAM_GEMM_SILU_MUL_CAT 2
 int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N, int K,
               int epilogue, int dtype, cram_stream_t stream);
+
+/*
+ * The q | k | v projection with RoPE in its epilogue (LlamaAttention.forward's q_proj / k_proj / v_proj followed by
+ * apply_rotary_pos_emb, re_weighting.py:158,170 via the hooked forward): cram_gemm with N = (hq + 2 hkv) * d, then
+ * on the rounded projection exactly cram_rope_split's arithmetic, table row pos[m] (or m % T):
+ *   kout == vout == NULL: cram_rope_inplace over the q and k heads (v heads stored as computed), all in out;
+ *   otherwise cram_rope_split: q rotated into out, k rotated into kout, v copied into vout; buffer row m < rows goes
+ *   to sequence m / T, row kv_row0 + m % T, or with dst_b to dst_b[m], kv_row0 + pos[m] (strides kv_bs / kv_hs /
+ *   kv_rs, elements); the k / v columns of out hold the rotated k and v if keep_k, else they are not written.
+ * Rows in [rows, M) are GEMM padding: out rows written (q), nothing else.  bf16, d = 128, K % 64 == 0, K >= 128
+ * (the 4-wave kernel), ldo % 8 == 0; pos / dst_b int64 device arrays of >= rows entries.  No bias (Llama).
+ */
+int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int K,
+                   int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t, int64_t tab_rs,
+                   const int64_t* pos, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs, int64_t kv_rs,
+                   int kv_row0, const int64_t* dst_b, int keep_k, int dtype, cram_stream_t stream);
+
+/*
+ * The same GEMM with the decoder layer's residual add in its epilogue (o_proj and down_proj: the residual
+ * stream h = h + o_proj(a), h = h + down(act) of LlamaDecoderLayer.forward, re_weighting.py:158,170 via the hooked
+ * forward): out[m, n] = rnd(res[m, n] + rnd(sum_k y[m, k] * x[n, k])) -- the bf16 add HF runs after the projection.
+ * res [M][N] (row stride ldr) may be out itself (same pointer and stride); any other overlap is CRAM_ERR_INVALID_ARG.
+ * Requirements of cram_gemm plus ldo % 8 == 0, ldr % 8 == 0 and a 16-byte aligned res.
+ */
+int cram_gemm_residual(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* res, int64_t ldr, void* out,
+                       int64_t ldo, int M, int N, int K, int dtype, cram_stream_t stream);
 
 /*
  * Split-K form of the same GEMM for the decode step's projections (few activation rows, M = the batch: 256 at

@@ -18,7 +18,7 @@ def test_header_declares_the_boundary():
     names = _declared()
     for n in ("cram_attn_prefill", "cram_attn_decode", "cram_attn_decode_workspace_size", "cram_answer_logits",
               "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_rope_split", "cram_silu_mul",
-              "cram_gemm"):
+              "cram_gemm", "cram_gemm_residual", "cram_gemm_rope"):
         assert n in names
 
 
@@ -30,7 +30,7 @@ def test_library_builds_loads_and_exports_every_symbol():
         assert hasattr(lib, n), n
     assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
     L = _lib.load()
-    assert L.cram_abi_version() == _lib.ABI_VERSION == 4
+    assert L.cram_abi_version() == _lib.ABI_VERSION == 5
     assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0
@@ -65,6 +65,29 @@ def test_argument_validation_without_gpu():
     assert L.cram_gemm(fake, 68, fake, 64, fake, 256, 1, 256, 64, 0, 0, None) == -3
     assert L.cram_gemm(fake, 64, fake, 64, fake, 256, 1, 256, 64, 2, 0, None) == -1
     assert L.cram_gemm(fake, 64, fake, 64, fake, 128, 1, 512, 64, 0, 0, None) == -1
+    # residual GEMM: residual presence and alignment, overlap other than exact aliasing, then cram_gemm's checks
+    far = 1 << 24
+    assert L.cram_gemm_residual(fake, 64, fake, 64, None, 256, fake, 256, 1, 256, 64, 0, None) == -1
+    assert L.cram_gemm_residual(fake, 64, fake, 64, far, 260, fake, 256, 1, 256, 64, 0, None) == -3
+    assert L.cram_gemm_residual(fake, 64, fake, 64, far + 8, 256, fake, 256, 1, 256, 64, 0, None) == -3
+    assert L.cram_gemm_residual(fake, 64, fake, 64, fake + 16, 256, fake, 256, 1, 256, 64, 0, None) == -1
+    assert L.cram_gemm_residual(fake, 64, fake, 64, far, 256, fake, 256, 0, 256, 64, 0, None) == -1
+    assert L.cram_gemm_residual(fake, 64, fake, 64, far, 256, fake, 256, 1, 200, 64, 0, None) == -2
+    assert L.cram_gemm_residual(fake, 64, fake, 64, fake, 256, fake, 256, 1, 256, 48, 0, None) == -2
+    # q/k/v + RoPE GEMM: tables, rows <= M, kout / vout together, dst_b needs pos, bf16 and head dim 128 only
+    def rope(M=256, K=128, rows=256, T=256, d=128, cos=fake, kout=None, vout=None, dst_b=None, pos=None, dtype=0,
+             ldo=6144):
+        return L.cram_gemm_rope(fake, K, fake, K, fake, ldo, M, K, rows, T, 32, 8, d, cos, fake, 128, pos, kout, vout,
+                                0, 0, 0, 0, dst_b, 0, dtype, None)
+    assert rope(cos=None) == -1
+    assert rope(rows=257) == -1
+    assert rope(kout=fake) == -1
+    assert rope(kout=fake, vout=fake, dst_b=fake) == -1
+    assert rope(kout=fake, vout=fake, rows=200, T=64) == -1
+    assert rope(d=64) == -2
+    assert rope(dtype=1) == -2
+    assert rope(K=64) == -2
+    assert rope(ldo=6148) == -3
     # split-K GEMM: K % (64 * splits), epilogue, bias only with STORE, workspace presence and size
     ws = L.cram_gemm_splitk_workspace_size(16, 512, 4)
     assert ws == 4 * 16 * 512 * 4

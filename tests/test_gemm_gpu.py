@@ -193,3 +193,184 @@ def test_engine_fused_mlp_matches_library_pair(gpu_device):
     d2 = (fused2.float() - lib2.float()).abs()
     assert d2.mean().item() <= 0.01 * lib2.float().abs().mean().item()
     assert not torch.equal(fused2, fused)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 64), (77, 512, 128), (300, 768, 4096), (4097, 1536, 4096),
+                                   (513, 256, 14336)])
+def test_gemm_residual_epilogue(gpu_device, gemm_variant, dtype, M, N, K):
+    """cram_gemm_residual (o_proj / down_proj with the decoder layer's residual add): out = rnd(res + rnd(acc)),
+    bit-identical to the same kernel's plain GEMM followed by a model-dtype add (HF's `residual + hidden_states`);
+    in place (out = res) gives the same bits."""
+    x, w = _operands(M, N, K, dtype, gpu_device, 13 * M + N + K)
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    res = ((torch.rand(M, N, generator=g) * 8 - 4).to(dtype)).to(gpu_device)
+    out = ops.gemm(x, w, residual=res)
+    exp = ops.gemm(x, w) + res                   # bf16 / fp16 add: fp32 sum of the two, rounded once
+    inplace = res.clone()
+    ops.gemm(x, w, residual=inplace, out=inplace)
+    ref = x.float() @ w.float().t() + res.float()
+    torch.cuda.synchronize()
+    assert out.shape == (M, N) and torch.isfinite(out.float()).all()
+    assert torch.equal(out, exp)
+    assert torch.equal(inplace, out)
+    acc_tol = 2.0 ** -22 * (x.float().abs() @ w.float().abs().t())
+    d = (out.float() - ref).abs()
+    # two roundings (the product, then the sum): within 1 ulp of the product plus 1 ulp of the sum
+    bar = _ulp(ref - res.float(), dtype) + _ulp(ref, dtype) + acc_tol
+    assert (d <= bar).all(), f"max err {d.max().item():.3e}"
+
+
+def test_gemm_residual_strided_rows_and_tail(gpu_device, gemm_variant):
+    """Residual and output as views into wider buffers, M not a multiple of the 256-row tile: nothing outside the
+    [M][N] output view is written."""
+    M, N, K = 333, 512, 256
+    x, w = _operands(M, N, K, torch.bfloat16, gpu_device, 17)
+    rbig = torch.randn(M, N + 64, device=gpu_device).to(torch.bfloat16)
+    res = rbig[:, 64:]
+    big = torch.full((M + 7, N + 128), 7.0, dtype=torch.bfloat16, device=gpu_device)
+    out = big[:M, 64:64 + N]
+    ops.gemm(x, w, out=out, residual=res)
+    exp = ops.gemm(x, w) + res
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp)
+    assert (big[M:] == 7).all() and (big[:M, :64] == 7).all() and (big[:M, 64 + N:] == 7).all()
+
+
+def test_engine_fused_residual_layer_matches_deferred_add(gpu_device):
+    """CrAMEngine.o_proj_norm / mlp_residual at sweep row counts (residual adds in the o_proj / down_proj epilogues)
+    == the deferred-add path (F.linear, the add inside the next RMSNorm) within the bf16 noise of two GEMM
+    accumulation orders; with the same GEMM on both sides the layer output is bit-identical."""
+    from cram_amd import engine as E
+    sp = E.ModelSpec(1, 1024, 8, 2, 128, 1536, 1000, 1e-5, False)
+    eng = E.CrAMEngine.random(sp, gpu_device, seed=12, std=0.03)
+    lw = eng.layers[0]
+    gen = torch.Generator(device=gpu_device).manual_seed(4)
+    a = torch.randn(4608, sp.q_size, device=gpu_device, generator=gen).to(torch.bfloat16)
+    h = torch.randn(4608, sp.hidden, device=gpu_device, generator=gen).to(torch.bfloat16)
+    assert eng._fused_residual_ok(a)
+    h2, x2 = eng.o_proj_norm(a, lw, h)
+    hout, m = eng.mlp_residual(x2, lw, h2)
+    assert m is None
+    # the same arithmetic with the add outside the GEMMs (cram_gemm both times: identical accumulation)
+    h2_ref, x2_ref = ops.rmsnorm(ops.gemm(a, lw.wo), lw.ln2, sp.eps, residual=h)
+    act = ops.gemm(x2_ref, eng._gate_up_interleaved(lw), ops.GEMM_SILU_MUL)
+    hout_ref = h2_ref + ops.gemm(act, lw.wd)
+    prev = E.FUSED_RESIDUAL
+    E.FUSED_RESIDUAL = False
+    try:
+        h2_lib, x2_lib = eng.o_proj_norm(a, lw, h)
+        hl, ml = eng.mlp_residual(x2_lib, lw, h2_lib)
+    finally:
+        E.FUSED_RESIDUAL = prev
+    torch.cuda.synchronize()
+    assert torch.equal(h2, h2_ref) and torch.equal(x2, x2_ref) and torch.equal(hout, hout_ref)
+    lib = hl + ml
+    d = (hout.float() - lib.float()).abs()
+    scale = lib.float().abs().mean().item()
+    assert d.max().item() <= 0.05 * lib.float().abs().max().item() and d.mean().item() <= 0.01 * scale, (d.max(), scale)
+
+
+def _rope_tables(P, d, dev, theta=500000.0):
+    inv = 1.0 / theta ** (torch.arange(0, d, 2, dtype=torch.float32) / d)
+    f = torch.arange(P, dtype=torch.float32)[:, None] * inv[None]
+    emb = torch.cat((f, f), -1)
+    return emb.cos().to(torch.bfloat16).to(dev), emb.sin().to(torch.bfloat16).to(dev)
+
+
+HQ, HKV, HD = 32, 8, 128
+
+
+@pytest.mark.parametrize("K", [256, 4096])
+def test_gemm_rope_inplace_equals_gemm_then_rope(gpu_device, K):
+    """cram_gemm_rope without kout (the sweep's suffix layers when no prefix is shared): bit-identical to the same
+    kernel's plain GEMM followed by cram_rope_inplace over the q and k heads; v heads as computed; GEMM padding rows
+    [rows, M) read table row 0 and are never compared."""
+    B, T = 3, 1000
+    rows, M = B * T, 3072
+    x, w = _operands(M, (HQ + 2 * HKV) * HD, K, torch.bfloat16, gpu_device, 41 + K)
+    cos, sin = _rope_tables(T, HD, gpu_device)
+    out = ops.gemm_rope(x, w, HQ, HKV, HD, cos, sin, T, rows=rows)
+    ref = ops.gemm(x, w)
+    ops.rope_inplace(ref[:rows], HQ + HKV, HD, cos, sin, T=T)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:rows], ref[:rows])
+
+
+def test_gemm_rope_split_behind_prefix(gpu_device):
+    """The sweep's layer_rows with a shared prefix: q rotated in place, k rotated into and v copied into the
+    [B, p0 + T] key / value buffers behind the prefix at table rows pos = p0 + t; == GEMM + cram_rope_split, the
+    prefix rows untouched, nothing written for the GEMM padding rows."""
+    B, T, p0 = 5, 700, 25
+    rows = B * T
+    M = 3584
+    x, w = _operands(M, (HQ + 2 * HKV) * HD, 512, torch.bfloat16, gpu_device, 43)
+    cos, sin = _rope_tables(p0 + T, HD, gpu_device)
+    pos = (torch.arange(T, device=gpu_device, dtype=torch.int64) + p0).repeat(B)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    k0 = torch.randn(B, p0 + T + 3, HKV, HD, generator=g).to(torch.bfloat16).to(gpu_device)
+    v0 = torch.randn(B, p0 + T + 3, HKV, HD, generator=g).to(torch.bfloat16).to(gpu_device)
+    k, v, kr, vr = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    out = ops.gemm_rope(x, w, HQ, HKV, HD, cos, sin, T, rows=rows, kout=k, vout=v, row0=p0, pos=pos)
+    ref = ops.gemm(x, w)
+    ops.rope_split(ref[:rows], HQ, HKV, HD, cos, sin, T, kr, vr, p0, pos=pos)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:rows, :HQ * HD], ref[:rows, :HQ * HD])
+    assert torch.equal(k, kr) and torch.equal(v, vr)
+    assert torch.equal(k[:, :p0], k0[:, :p0]) and torch.equal(k[:, p0 + T:], k0[:, p0 + T:])
+
+
+def test_gemm_rope_split_into_cache_keep_k(gpu_device):
+    """The packed decode prefill: ragged sequences packed row after row, K/V scattered into the cache
+    ([B, Hkv, S, d] seen as [B, S, Hkv, d]) at (dst_b[m], pos[m]); keep_k leaves the rotated k and v in the buffer
+    for the varlen attention; == GEMM + cram_rope_split(keep_k)."""
+    lens = [300, 1, 777, 64, 1000]
+    total = sum(lens)
+    M = 2304
+    S = 1024
+    x, w = _operands(M, (HQ + 2 * HKV) * HD, 256, torch.bfloat16, gpu_device, 47)
+    cos, sin = _rope_tables(S, HD, gpu_device)
+    pos = torch.cat([torch.arange(n, dtype=torch.long) for n in lens]).to(gpu_device)
+    bidx = torch.cat([torch.full((n,), b, dtype=torch.long) for b, n in enumerate(lens)]).to(gpu_device)
+    kc = torch.zeros(len(lens), HKV, S, HD, dtype=torch.bfloat16, device=gpu_device)
+    vc = torch.zeros_like(kc)
+    kcr, vcr = kc.clone(), vc.clone()
+    out = ops.gemm_rope(x, w, HQ, HKV, HD, cos, sin, 1, rows=total, kout=kc.transpose(1, 2),
+                        vout=vc.transpose(1, 2), row0=0, pos=pos, dst_b=bidx, keep_k=True)
+    ref = ops.gemm(x, w)
+    ops.rope_split(ref[:total], HQ, HKV, HD, cos, sin, 1, kcr.transpose(1, 2), vcr.transpose(1, 2), 0, pos=pos,
+                   dst_b=bidx, keep_k=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:total], ref[:total])
+    assert torch.equal(kc, kcr) and torch.equal(vc, vcr)
+
+
+def test_engine_fused_qkv_layer_matches_library_path(gpu_device):
+    """CrAMEngine.layer_rows at sweep row counts with RoPE in the q/k/v GEMM's epilogue == the library path
+    (hipBLASLt + cram_rope_split) within the bf16 noise of two GEMM accumulation orders, with and without a shared
+    prefix."""
+    from cram_amd import engine as E
+    sp = E.ModelSpec(2, 1024, 8, 2, 128, 1536, 1000, 1e-5, False)
+    eng = E.CrAMEngine.random(sp, gpu_device, seed=13, std=0.03)
+    B, T, p0 = 9, 500, 20
+    gen = torch.Generator(device=gpu_device).manual_seed(5)
+    h = torch.randn(B * T, sp.hidden, device=gpu_device, generator=gen).to(torch.bfloat16)
+    cos, sin = eng.rope_tables(p0 + T)
+    k0 = torch.randn(1, p0, sp.num_kv_heads, sp.head_dim, device=gpu_device, generator=gen).to(torch.bfloat16)
+    v0 = torch.randn_like(k0)
+    pos = (torch.arange(T, device=gpu_device, dtype=torch.int64) + p0).repeat(B)
+    assert eng._fused_qkv_ok(h, eng.layers[1])
+    for pre in (None, (k0, v0, pos)):
+        fused = eng.layer_rows(h, B, T, 1, cos, sin, prefix=pre)
+        prev = E.FUSED_QKV
+        E.FUSED_QKV = False
+        try:
+            lib = eng.layer_rows(h, B, T, 1, cos, sin, prefix=pre)
+        finally:
+            E.FUSED_QKV = prev
+        torch.cuda.synchronize()
+        of = fused[0] if fused[1] is None else fused[0] + fused[1]
+        ol = lib[0] if lib[1] is None else lib[0] + lib[1]
+        d = (of.float() - ol.float()).abs()
+        scale = ol.float().abs().mean().item()
+        assert d.max().item() <= 0.05 * ol.float().abs().max().item() and d.mean().item() <= 0.01 * scale
