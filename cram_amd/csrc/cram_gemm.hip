@@ -104,7 +104,7 @@ struct GemmParams {
   const void* res; int64_t ldr;    // EPI_RESIDUAL: the residual stream [M, N] (may be out itself)
   // EPI_ROPE (head dim 128; a wave's 128 output columns are one head): see cram_gemm_rope in cram_attn.h
   const void* cos_t; const void* sin_t; int64_t tab_rs;
-  const int64_t* pos; const int64_t* dst_b;
+  const int64_t* pos; const int64_t* dst_b; int64_t pos0;
   void* kout; void* vout; int64_t kv_bs, kv_hs, kv_rs;
   int rows, T, hq, hkv, kv_row0, keep_k;
   int M, N, K;
@@ -529,7 +529,6 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   // vout (with keep_k the k and v heads also stay in out); without kout every head goes to out (q, k rotated)
   const int hidx = (n0 + 128 * wn) >> 7;
   const int kind = EPI != EPI_ROPE ? 0 : (hidx < p.hq ? 0 : (hidx < p.hq + p.hkv ? 1 : 2));
-  const bool rot = EPI == EPI_ROPE && kind < 2;
   V8 rv[EPI == EPI_RESIDUAL ? NRB : 1];
   if constexpr (EPI == EPI_RESIDUAL) {
     const T* rb = static_cast<const T*>(p.res);
@@ -546,36 +545,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
     constexpr int b = decltype(bi)::value;
     const int ml = 16 * b + fr;                  // the lane's row within the wave's 128
     const int sw = swz(ml);
-    bool staged = false;
-    if constexpr (EPI == EPI_ROPE) {
-      if (rot) {
-        // rotation pairs (c, c + 64) of the wave's head sit in the same lane: tiles a and a + 4, element i.
-        // rope_kernel's arithmetic on the rounded projection: x1' = rnd(rnd(x1 c1) + rnd(-x2 s1)),
-        // x2' = rnd(rnd(x2 c2) + rnd(x1 s2)), table row = pos[m] (or m % T)
-        const int m = mw + ml;
-        const int64_t pp = m < p.rows ? (p.pos ? p.pos[m] : (int64_t)(m % p.T)) : 0;
-        const T* ct = static_cast<const T*>(p.cos_t) + pp * p.tab_rs + 4 * fg;
-        const T* st = static_cast<const T*>(p.sin_t) + pp * p.tab_rs + 4 * fg;
-        static_for<4>([&](auto ai) {
-          constexpr int a = decltype(ai)::value;
-          const V4 c1 = *reinterpret_cast<const V4*>(ct + 16 * a), c2 = *reinterpret_cast<const V4*>(ct + 64 + 16 * a);
-          const V4 s1 = *reinterpret_cast<const V4*>(st + 16 * a), s2 = *reinterpret_cast<const V4*>(st + 64 + 16 * a);
-          const f32x4 v1 = acc4<4 * (8 * a + b)>(), v2 = acc4<4 * (8 * (a + 4) + b)>();
-          V4 o1, o2;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float x1 = rnd<T>(v1[i]), x2 = rnd<T>(v2[i]);
-            o1[i] = (T)(rnd<T>(x1 * (float)c1[i]) + rnd<T>(-x2 * (float)s1[i]));
-            o2[i] = (T)(rnd<T>(x2 * (float)c2[i]) + rnd<T>(x1 * (float)s2[i]));
-          }
-          *reinterpret_cast<V4*>(wl + ml * RB + (((4 * a + fg) ^ sw) * 8)) = o1;
-          *reinterpret_cast<V4*>(wl + ml * RB + (((4 * (a + 4) + fg) ^ sw) * 8)) = o2;
-        });
-        staged = true;
-      }
-    }
-    if (staged) {
-    } else if constexpr (ROWS) {
+    if constexpr (ROWS) {
       static_for<8>([&](auto ai) {
         constexpr int a = decltype(ai)::value;
         const f32x4 v = acc4<4 * (8 * a + b)>();
@@ -613,20 +583,70 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
       if (mw + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mw + ml) * p.ldo + col0) = v;
     }
   } else if constexpr (EPI == EPI_ROPE) {
+    // read-back by rotation pairs: 8 lanes per row, lane c holds columns 8c.. and 64 + 8c.. of the wave's head;
+    // rope_kernel's arithmetic on the staged (rounded) projection, x1' = rnd(rnd(x1 c1) + rnd(-x2 s1)),
+    // x2' = rnd(rnd(x2 c2) + rnd(x1 s2)), table row pos[m] (or pos0 + m % T).  Rows go in groups of 4
+    // instructions whose table / index loads are all issued before the group's first use (one wait per group).
+    const bool rot = kind < 2;
     const bool split = p.kout != nullptr;
     const bool to_out = !split || kind == 0 || p.keep_k;        // keep_k: the k / v heads stay in out too
+    const bool to_kv = split && kind != 0;
+    const int c8 = lane & 7, r8 = lane >> 3;
     T* const kvb = static_cast<T*>(kind == 2 ? p.vout : p.kout) +
-                   (int64_t)(hidx - p.hq - (kind == 2 ? p.hkv : 0)) * p.kv_hs + 8 * cl;
-#pragma unroll 4
-    for (int j = 0; j < NRB; ++j) {
-      const int ml = RPI * j + rl;
-      const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
-      const int m = mw + ml;
-      if (to_out && m < p.M) *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + col0) = v;
-      if (split && kind != 0 && m < p.rows) {
-        const int64_t sb = p.dst_b ? p.dst_b[m] : (int64_t)(m / p.T);
-        const int64_t t = p.dst_b ? p.pos[m] : (int64_t)(m % p.T);
-        *reinterpret_cast<V8*>(kvb + sb * p.kv_bs + (p.kv_row0 + t) * p.kv_rs) = v;
+                   (int64_t)(hidx - p.hq - (kind == 2 ? p.hkv : 0)) * p.kv_hs + 8 * c8;
+    const int64_t colw = (int64_t)n0 + 128 * wn + 8 * c8;
+    const T* const cosb = static_cast<const T*>(p.cos_t) + 8 * c8;
+    const T* const sinb = static_cast<const T*>(p.sin_t) + 8 * c8;
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {
+      int64_t tp[4], kd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = mw + 8 * (4 * g + u) + r8;
+        const bool live = m < p.rows;
+        tp[u] = !live ? 0 : (p.pos ? p.pos[m] : p.pos0 + (int64_t)(m % p.T));
+        kd[u] = 0;
+        if (to_kv && live) {
+          const int64_t sb = p.dst_b ? p.dst_b[m] : (int64_t)(m / p.T);
+          const int64_t t = p.dst_b ? tp[u] : (int64_t)(m % p.T);
+          kd[u] = sb * p.kv_bs + (p.kv_row0 + t) * p.kv_rs;
+        }
+      }
+      V8 c1[4], c2[4], s1[4], s2[4];
+      if (rot) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          c1[u] = *reinterpret_cast<const V8*>(cosb + tp[u] * p.tab_rs);
+          c2[u] = *reinterpret_cast<const V8*>(cosb + tp[u] * p.tab_rs + 64);
+          s1[u] = *reinterpret_cast<const V8*>(sinb + tp[u] * p.tab_rs);
+          s2[u] = *reinterpret_cast<const V8*>(sinb + tp[u] * p.tab_rs + 64);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ml = 8 * (4 * g + u) + r8;
+        const int m = mw + ml;
+        V8 x1 = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * c8) ^ swz(ml)) * 8));
+        V8 x2 = *reinterpret_cast<const V8*>(wl + ml * RB + (((16 + 2 * c8) ^ swz(ml)) * 8));
+        if (rot) {
+          V8 o1, o2;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float a = (float)x1[i], b = (float)x2[i];
+            o1[i] = (T)(rnd<T>(a * (float)c1[u][i]) + rnd<T>(-b * (float)s1[u][i]));
+            o2[i] = (T)(rnd<T>(b * (float)c2[u][i]) + rnd<T>(a * (float)s2[u][i]));
+          }
+          x1 = o1;
+          x2 = o2;
+        }
+        if (to_out && m < p.M) {
+          *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + colw) = x1;
+          *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + colw + 64) = x2;
+        }
+        if (to_kv && m < p.rows) {
+          *reinterpret_cast<V8*>(kvb + kd[u]) = x1;
+          *reinterpret_cast<V8*>(kvb + kd[u] + 64) = x2;
+        }
       }
     }
   } else {
@@ -775,10 +795,11 @@ extern "C" int cram_gemm_residual(const void* y, int64_t ldy, const void* x, int
 
 extern "C" int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M,
                               int K, int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t,
-                              int64_t tab_rs, const int64_t* pos, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs,
+                              int64_t tab_rs, const int64_t* pos, int pos0, void* kout, void* vout, int64_t kv_bs,
+                              int64_t kv_hs,
                               int64_t kv_rs, int kv_row0, const int64_t* dst_b, int keep_k, int dtype,
                               cram_stream_t stream) {
-  if (!cos_t || !sin_t || rows < 0 || rows > M || T <= 0 || hq <= 0 || hkv <= 0 || kv_row0 < 0)
+  if (!cos_t || !sin_t || rows < 0 || rows > M || T <= 0 || hq <= 0 || hkv <= 0 || kv_row0 < 0 || pos0 < 0)
     return CRAM_ERR_INVALID_ARG;
   if ((kout == nullptr) != (vout == nullptr) || (dst_b && !pos) || (kout && !dst_b && rows % T != 0))
     return CRAM_ERR_INVALID_ARG;
@@ -788,7 +809,7 @@ extern "C" int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t
   GemmParams p{};
   p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = out; p.ldo = ldo;
   p.M = M; p.N = (hq + 2 * hkv) * d; p.K = K;
-  p.cos_t = cos_t; p.sin_t = sin_t; p.tab_rs = tab_rs; p.pos = pos; p.dst_b = dst_b;
+  p.cos_t = cos_t; p.sin_t = sin_t; p.tab_rs = tab_rs; p.pos = pos; p.pos0 = pos0; p.dst_b = dst_b;
   p.kout = kout; p.vout = vout; p.kv_bs = kv_bs; p.kv_hs = kv_hs; p.kv_rs = kv_rs;
   p.rows = rows; p.T = T; p.hq = hq; p.hkv = hkv; p.kv_row0 = kv_row0; p.keep_k = keep_k;
   return gemm_launch(p, EPI_ROPE, dtype, (hipStream_t)stream);

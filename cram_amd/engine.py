@@ -360,8 +360,9 @@ class CrAMEngine:
             v[:, :p0] = v0
             # q roped in place; the suffix's roped k and its v land behind the prefix (no copy pass)
             if fused:
+                # the suffix rows' positions are p0 + t (the pos array's content): no position loads
                 y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M,
-                                  kout=k, vout=v, row0=p0, pos=pos)
+                                  kout=k, vout=v, row0=p0, pos0=p0)
             else:
                 y = ops.linear(x, lw.wqkv, lw.bqkv)
                 ops.rope_split(y[:M], sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)

@@ -420,10 +420,11 @@ def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int
               sin: torch.Tensor, T: int, rows: Optional[int] = None, kout: Optional[torch.Tensor] = None,
               vout: Optional[torch.Tensor] = None, row0: int = 0, pos: Optional[torch.Tensor] = None,
               dst_b: Optional[torch.Tensor] = None, keep_k: bool = False, out: Optional[torch.Tensor] = None,
-              name: str = "cram_gemm") -> torch.Tensor:
+              pos0: int = 0, name: str = "cram_gemm") -> torch.Tensor:
     """The q | k | v projection x @ w^T with RoPE in the GEMM epilogue (cram_gemm_rope, the 4-wave kernel; bf16,
     head_dim 128, no bias).  Without kout / vout: ``rope_inplace`` over the q and k heads of the result (T, pos as
-    there).  With them: ``rope_split`` into kout / vout ([B, S, hkv, d] views, row0, pos, dst_b, keep_k as there),
+    there; without pos the table row is pos0 + m % T).  With them: ``rope_split`` into kout / vout ([B, S, hkv, d]
+    views, row0, pos, dst_b, keep_k as there),
     for the first ``rows`` rows of x (default all; rows beyond are GEMM padding).  Returns the [M, N] buffer: q
     rotated; k rotated and v as computed unless kout is given without keep_k (then those columns are not written)."""
     _dt(x)
@@ -460,7 +461,7 @@ def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int
     st = (0, 0, 0) if kout is None else (kout.stride(0), kout.stride(2), kout.stride(1))
     code = _lib.load().cram_gemm_rope(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
                                       o2.stride(0), M, K, rows, int(T), int(hq), int(hkv), int(head_dim),
-                                      cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), _ptr(kout),
+                                      cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), int(pos0), _ptr(kout),
                                       _ptr(vout), st[0], st[1], st[2], int(row0), _ptr(dst_b), int(bool(keep_k)),
                                       _dt(x), _stream(x.device))
     _lib.check(code, "cram_gemm_rope")

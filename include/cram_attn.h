@@ -203,7 +203,8 @@ int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out,
 /*
  * The q | k | v projection with RoPE in its epilogue (LlamaAttention.forward's q_proj / k_proj / v_proj followed by
  * apply_rotary_pos_emb, re_weighting.py:158,170 via the hooked forward): cram_gemm with N = (hq + 2 hkv) * d, then
- * on the rounded projection exactly cram_rope_split's arithmetic, table row pos[m] (or m % T):
+ * on the rounded projection exactly cram_rope_split's arithmetic, table row pos[m] (or pos0 + m % T: the IE
+ * sweep's suffix rows, whose positions continue a shared prefix of pos0 tokens, need no position array):
  *   kout == vout == NULL: cram_rope_inplace over the q and k heads (v heads stored as computed), all in out;
  *   otherwise cram_rope_split: q rotated into out, k rotated into kout, v copied into vout; buffer row m < rows goes
  *   to sequence m / T, row kv_row0 + m % T, or with dst_b to dst_b[m], kv_row0 + pos[m] (strides kv_bs / kv_hs /
@@ -213,7 +214,7 @@ int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out,
  */
 int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int K,
                    int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t, int64_t tab_rs,
-                   const int64_t* pos, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs, int64_t kv_rs,
+                   const int64_t* pos, int pos0, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs, int64_t kv_rs,
                    int kv_row0, const int64_t* dst_b, int keep_k, int dtype, cram_stream_t stream);
 
 /*

@@ -10,6 +10,7 @@
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (config 3 + decode, CPU baselines)
 #   bench:ARGS       bench.py with ARGS (commas become spaces), e.g. bench:--config,2,--no-cpu-baseline
+#   benv:ENV:ARGS    bench.py ARGS under ENV (NAME=V pairs joined by +), e.g. benv:CRAM_FUSED_QKV=0:--no-decode (A/B arms)
 #   prof             rocprofv3 --kernel-trace --stats of the sweep-only bench (summary kept, traces deleted)
 #   pmc              the attention kernel's PMC passes (tools/pmc_attn.sh) -> pmc_summary.txt + attn_pmc.json
 #   test:PATTERN     pytest -m gpu -k PATTERN
@@ -34,6 +35,9 @@ for step in "$@"; do
     bench:*)   a=${step#bench:}; n=$(echo "$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
                timeout -k 10 900 python -u bench.py ${a//,/ } > $O/bench_$n.json 2> $O/bench_$n.err
                head -c 700 $O/bench_$n.json; echo ;;
+    benv:*)    a=${step#benv:}; e=${a%%:*}; a=${a#*:}; n=$(echo "$e$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-70)
+               timeout -k 10 900 env ${e//+/ } python -u bench.py ${a//,/ } > $O/benv_$n.json 2> $O/benv_$n.err
+               head -c 400 $O/benv_$n.json; echo ;;
     prof)      mkdir -p $O/prof
                timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o sweep \
                  -- python3 bench.py --no-cpu-baseline --no-decode > $O/prof/sweep.json 2> $O/prof/sweep.err
