@@ -75,6 +75,8 @@ SIGNATURES = {
     "cram_gemm_splitk_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cram_gemm_splitk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int,
                                  c_int, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "cram_gemm_splitk_residual": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64,
+                                          c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_int, c_void_p]),
     "cram_passage_weights": (c_int, [c_int] + [c_void_p] * 9),
 }
 

@@ -666,10 +666,10 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
 //                           out[m, f] = rnd(rnd(silu(rnd(g))) * rnd(u)), g = sum[m, f], u = sum[m, F + f]
 template <typename T, int EPI>
 __global__ __launch_bounds__(256) void gemm_combine_kernel(const float* __restrict__ part, int splits, int M, int N,
-                                                           const T* __restrict__ bias, T* __restrict__ out,
-                                                           int64_t ldo) {
+                                                           const T* __restrict__ bias, const T* __restrict__ res,
+                                                           int64_t ldr, T* __restrict__ out, int64_t ldo) {
   using V4 = typename GVec<T>::x4;
-  const int nout = EPI == CRAM_GEMM_STORE ? N : N / 2;
+  const int nout = EPI == CRAM_GEMM_SILU_MUL_CAT ? N / 2 : N;
   const unsigned vpr = (unsigned)nout >> 3;
   const unsigned gid = blockIdx.x * 256u + threadIdx.x;      // host guarantees M * vpr < 2^31
   if (gid >= (unsigned)M * vpr) return;
@@ -698,6 +698,8 @@ __global__ __launch_bounds__(256) void gemm_combine_kernel(const float* __restri
     float r;
     if constexpr (EPI == CRAM_GEMM_STORE) {
       r = bias ? a[j] + (float)bias[c + j] : a[j];
+    } else if constexpr (EPI == EPI_RESIDUAL) {
+      r = (float)res[(int64_t)m * ldr + c + j] + rnd<T>(a[j]);
     } else {
       const float g = rnd<T>(a[j]);
       r = rnd<T>(g / (1.0f + expf(-g))) * rnd<T>(u[j]);
@@ -820,22 +822,24 @@ extern "C" size_t cram_gemm_splitk_workspace_size(int M, int N, int splits) {
   return (size_t)splits * (size_t)M * (size_t)N * sizeof(float);
 }
 
-extern "C" int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo,
-                                int M, int N, int K, int splits, int epilogue, const void* bias, void* workspace,
-                                size_t ws_bytes, int dtype, cram_stream_t stream) {
+namespace {
+
+// cram_gemm_splitk / cram_gemm_splitk_residual: partial sums of every (tile, K range) on the 8-wave kernel, then the
+// range-ordered combine with the epilogue
+int splitk_launch(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N, int K,
+                  int splits, int epi, const void* bias, const void* res, int64_t ldr, void* workspace,
+                  size_t ws_bytes, int dtype, hipStream_t st) {
   if (!y || !x || !out || M <= 0 || N <= 0 || K <= 0 || splits <= 0) return CRAM_ERR_INVALID_ARG;
-  if (epilogue != CRAM_GEMM_STORE && epilogue != CRAM_GEMM_SILU_MUL_CAT) return CRAM_ERR_INVALID_ARG;
-  if (bias && epilogue != CRAM_GEMM_STORE) return CRAM_ERR_INVALID_ARG;
   if (dtype != CRAM_DTYPE_BF16 && dtype != CRAM_DTYPE_F16) return CRAM_ERR_UNSUPPORTED;
   if (N % BN != 0 || K % (BK * splits) != 0) return CRAM_ERR_UNSUPPORTED;
   if (!al16(y) || !al16(x) || !al16(out) || (ldy & 7) || (ldx & 7) || (ldo & 7)) return CRAM_ERR_ALIGNMENT;
   if (bias && (reinterpret_cast<uintptr_t>(bias) & 15u)) return CRAM_ERR_ALIGNMENT;
-  const int nout = epilogue == CRAM_GEMM_STORE ? N : N / 2;
+  const int nout = epi == CRAM_GEMM_SILU_MUL_CAT ? N / 2 : N;
   if (ldy < K || ldx < K || ldo < nout) return CRAM_ERR_INVALID_ARG;
   if ((int64_t)BN * ldx * 2 >= (1ll << 31) || (int64_t)BM * ldy * 2 >= (1ll << 31)) return CRAM_ERR_UNSUPPORTED;
   if (!workspace || ws_bytes < cram_gemm_splitk_workspace_size(M, N, splits)) return CRAM_ERR_WORKSPACE;
   if ((reinterpret_cast<uintptr_t>(workspace) & 15u)) return CRAM_ERR_ALIGNMENT;
-  GemmParams p;
+  GemmParams p{};
   p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy; p.out = workspace; p.ldo = N;
   p.M = M; p.N = N; p.K = K;
   p.splits = splits; p.kts = K / (BK * splits); p.raster = 0;
@@ -845,24 +849,52 @@ extern "C" int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64
   const int64_t nvec = (int64_t)M * (nout / 8);
   if (nb > 0x7fffffff || nvec >= (1ll << 31)) return CRAM_ERR_INVALID_ARG;
   p.nblocks = (int)nb;
-  const hipStream_t st = (hipStream_t)stream;
   const dim3 gc((unsigned)((nvec + 255) / 256));
-  if (dtype == CRAM_DTYPE_BF16) {
-    hipLaunchKernelGGL((gemm_tn_kernel<__bf16, EPI_PARTIAL>), dim3(p.nblocks), dim3(512), 0, st, p);
-    if (epilogue == CRAM_GEMM_STORE)
-      hipLaunchKernelGGL((gemm_combine_kernel<__bf16, CRAM_GEMM_STORE>), gc, dim3(256), 0, st,
-                         (const float*)workspace, splits, M, N, (const __bf16*)bias, (__bf16*)out, ldo);
+  const float* ws = static_cast<const float*>(workspace);
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((gemm_tn_kernel<T, EPI_PARTIAL>), dim3(p.nblocks), dim3(512), 0, st, p);
+    const T* b = static_cast<const T*>(bias);
+    const T* r = static_cast<const T*>(res);
+    T* o = static_cast<T*>(out);
+    if (epi == CRAM_GEMM_STORE)
+      hipLaunchKernelGGL((gemm_combine_kernel<T, CRAM_GEMM_STORE>), gc, dim3(256), 0, st, ws, splits, M, N, b, r, ldr, o,
+                         ldo);
+    else if (epi == EPI_RESIDUAL)
+      hipLaunchKernelGGL((gemm_combine_kernel<T, EPI_RESIDUAL>), gc, dim3(256), 0, st, ws, splits, M, N, b, r, ldr, o,
+                         ldo);
     else
-      hipLaunchKernelGGL((gemm_combine_kernel<__bf16, CRAM_GEMM_SILU_MUL_CAT>), gc, dim3(256), 0, st,
-                         (const float*)workspace, splits, M, N, (const __bf16*)nullptr, (__bf16*)out, ldo);
-  } else {
-    hipLaunchKernelGGL((gemm_tn_kernel<_Float16, EPI_PARTIAL>), dim3(p.nblocks), dim3(512), 0, st, p);
-    if (epilogue == CRAM_GEMM_STORE)
-      hipLaunchKernelGGL((gemm_combine_kernel<_Float16, CRAM_GEMM_STORE>), gc, dim3(256), 0, st,
-                         (const float*)workspace, splits, M, N, (const _Float16*)bias, (_Float16*)out, ldo);
-    else
-      hipLaunchKernelGGL((gemm_combine_kernel<_Float16, CRAM_GEMM_SILU_MUL_CAT>), gc, dim3(256), 0, st,
-                         (const float*)workspace, splits, M, N, (const _Float16*)nullptr, (_Float16*)out, ldo);
-  }
+      hipLaunchKernelGGL((gemm_combine_kernel<T, CRAM_GEMM_SILU_MUL_CAT>), gc, dim3(256), 0, st, ws, splits, M, N, b, r,
+                         ldr, o, ldo);
+  };
+  if (dtype == CRAM_DTYPE_BF16) run(__bf16{});
+  else run(_Float16{});
   return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
+}
+
+}  // namespace
+
+extern "C" int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo,
+                                int M, int N, int K, int splits, int epilogue, const void* bias, void* workspace,
+                                size_t ws_bytes, int dtype, cram_stream_t stream) {
+  if (epilogue != CRAM_GEMM_STORE && epilogue != CRAM_GEMM_SILU_MUL_CAT) return CRAM_ERR_INVALID_ARG;
+  if (bias && epilogue != CRAM_GEMM_STORE) return CRAM_ERR_INVALID_ARG;
+  return splitk_launch(y, ldy, x, ldx, out, ldo, M, N, K, splits, epilogue, bias, nullptr, 0, workspace, ws_bytes,
+                       dtype, (hipStream_t)stream);
+}
+
+extern "C" int cram_gemm_splitk_residual(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* res,
+                                         int64_t ldr, void* out, int64_t ldo, int M, int N, int K, int splits,
+                                         void* workspace, size_t ws_bytes, int dtype, cram_stream_t stream) {
+  if (!res || M <= 0 || N <= 0) return CRAM_ERR_INVALID_ARG;
+  if (!al16(res) || (ldr & 7)) return CRAM_ERR_ALIGNMENT;
+  if (ldr < N) return CRAM_ERR_INVALID_ARG;
+  const char* r0 = static_cast<const char*>(res);
+  const char* o0 = static_cast<const char*>(out);
+  if (r0 != o0 || ldr != ldo) {                  // the residual may be out itself; no other overlap
+    const int64_t rspan = ((int64_t)(M - 1) * ldr + N) * 2, ospan = ((int64_t)(M - 1) * ldo + N) * 2;
+    if (r0 < o0 + ospan && o0 < r0 + rspan) return CRAM_ERR_INVALID_ARG;
+  }
+  return splitk_launch(y, ldy, x, ldx, out, ldo, M, N, K, splits, EPI_RESIDUAL, nullptr, res, ldr, workspace,
+                       ws_bytes, dtype, (hipStream_t)stream);
 }

@@ -88,6 +88,8 @@ FUSED_RESIDUAL = os.environ.get("CRAM_FUSED_RESIDUAL", "1") != "0"
 # q/k/v projection with RoPE in cram_gemm's epilogue (bf16, head_dim 128, no q/k/v bias) at the same row counts;
 # CRAM_FUSED_QKV=0: hipBLASLt + cram_rope_inplace / cram_rope_split (A/B)
 FUSED_QKV = os.environ.get("CRAM_FUSED_QKV", "1") != "0"
+# the sparse last wave of the residual GEMMs' tiles through split-K (CrAMEngine._gemm_residual); 0 = one launch (A/B)
+TAIL_SPLIT = os.environ.get("CRAM_TAIL_SPLIT", "1") != "0"
 # packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where hipBLASLt already runs at full rate
 PREFILL_CHUNK_ROWS = 32768
 
@@ -249,7 +251,7 @@ class CrAMEngine:
         counts the residual add runs in o_proj's epilogue (cram_gemm_residual) and the norm reads one tensor;
         otherwise o_proj is F.linear and the add runs inside the norm.  Same rounding points either way."""
         if self._fused_residual_ok(a):
-            h2 = ops.gemm(a, lw.wo, residual=h)
+            h2 = self._gemm_residual(a, lw.wo, h)
             return h2, ops.rmsnorm(h2, lw.ln2, self.spec.eps)
         return ops.rmsnorm(ops.linear(a, lw.wo), lw.ln2, self.spec.eps, residual=h)
 
@@ -259,7 +261,7 @@ class CrAMEngine:
         consumer's RMSNorm (its residual input)."""
         if self._fused_residual_ok(x):
             act = ops.gemm(x, self._gate_up_interleaved(lw), ops.GEMM_SILU_MUL)
-            return ops.gemm(act, lw.wd, residual=h), None
+            return self._gemm_residual(act, lw.wd, h), None
         return h, self.mlp(x, lw)
 
     # gate/up with the fused activation: bf16 (the 4-wave kernel's type), 256-row tiles filled, the weight interleaved
@@ -271,6 +273,36 @@ class CrAMEngine:
         D, F = self.spec.hidden, self.spec.intermediate
         M = x.numel() // x.shape[-1]
         return M >= self.FUSED_MLP_MIN_ROWS and (2 * F) % 256 == 0 and D % 64 == 0 and D >= 128
+
+    def _gemm_residual(self, x: torch.Tensor, w: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+        """h + x @ w^T on row buffers with the add in the GEMM epilogue.  The 4-wave kernel runs one 256 x 256 tile
+        per CU, so a launch takes ceil(tiles / CUs) tile times: at the sweep's row counts the N = 4096 projections'
+        last wave is often a few tiles (M = 29,184: 1,824 tiles = 7 waves + 32), and o_proj / down_proj (down: 3.5x
+        the K) then leave ~7/8 of the chip idle for a whole tile time.  Rows past the last whole wave go instead
+        through the split-K form with the same epilogue, their K cut into ranges until the tail fills the chip."""
+        M, K, N = x.numel() // x.shape[-1], x.shape[-1], w.shape[0]
+        ntn, mt = N // 256, -(-M // 256)
+        waves = mt * ntn // self.num_cus
+        mt_main = waves * self.num_cus // ntn
+        tail = (mt - mt_main) * ntn
+        if TAIL_SPLIT and waves >= 1 and 0 < tail <= self.num_cus // 2 and mt_main * 256 < M:
+            splits = 1
+            while (tail * splits * 2 <= self.num_cus and K % (64 * splits * 2) == 0
+                   and K // (64 * splits * 2) >= 4):
+                splits *= 2
+            if splits > 1:
+                Mm = mt_main * 256
+                out = torch.empty_like(h)
+                ops.gemm(x[:Mm], w, residual=h[:Mm], out=out[:Mm])
+                ops.gemm_splitk(x[Mm:M], w, splits, residual=h[Mm:M], out=out[Mm:M])
+                return out
+        return ops.gemm(x, w, residual=h)
+
+    @property
+    def num_cus(self) -> int:
+        if getattr(self, "_num_cus", None) is None:
+            self._num_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return self._num_cus
 
     def _fused_qkv_ok(self, x: torch.Tensor, lw: LayerW) -> bool:
         sp = self.spec

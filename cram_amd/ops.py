@@ -476,11 +476,13 @@ def gemm_splitk_workspace_bytes(M: int, N: int, splits: int) -> int:
 
 def gemm_splitk(x: torch.Tensor, w: torch.Tensor, splits: int, epilogue: int = GEMM_STORE,
                 bias: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
-                out: Optional[torch.Tensor] = None, name: str = "cram_gemm_splitk") -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, name: str = "cram_gemm_splitk",
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x [..., K] @ w[N, K]^T (+ bias) with K cut into `splits` ranges (cram_gemm_splitk: the decode step's skinny
     projections); GEMM_SILU_MUL_CAT takes the checkpoint's [gate; up] weight and returns the MLP activation
     [..., N/2].  workspace: a uint8 device tensor of >= gemm_splitk_workspace_bytes(M, N, splits) (allocated here
-    when None; pass one for hipGraph capture)."""
+    when None; pass one for hipGraph capture).  residual [..., N] (GEMM_STORE, no bias): returns residual + x @ w^T
+    with the add in the combine (cram_gemm_splitk_residual; `out` may be residual itself)."""
     _dt(x)
     if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
         raise ValueError("w must be a [N, K] row-major weight of x's dtype")
@@ -498,12 +500,27 @@ def gemm_splitk(x: torch.Tensor, w: torch.Tensor, splits: int, epilogue: int = G
     need = gemm_splitk_workspace_bytes(M, N, splits)
     if workspace is None:
         workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
-    ev = TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout), x.device) if TIMER.enabled else None
-    code = _lib.load().cram_gemm_splitk(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
-                                        o2.stride(0), M, N, K, int(splits), int(epilogue),
-                                        None if bias is None else bias.data_ptr(), workspace.data_ptr(),
-                                        workspace.numel(), _dt(x), _stream(x.device))
-    _lib.check(code, "cram_gemm_splitk")
+    if residual is not None:
+        if epilogue != GEMM_STORE or bias is not None or residual.dtype != x.dtype or residual.shape[-1] != N:
+            raise ValueError("residual must be a [..., N] tensor of x's dtype (GEMM_STORE, no bias)")
+        r2 = _rows2d(residual, "residual")
+        if r2.shape[0] != M:
+            raise ValueError(f"residual has {r2.shape[0]} rows, x has {M}")
+    rbytes = 0 if residual is None else 2.0 * M * N
+    ev = (TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout) + rbytes, x.device)
+          if TIMER.enabled else None)
+    if residual is None:
+        code = _lib.load().cram_gemm_splitk(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
+                                            o2.stride(0), M, N, K, int(splits), int(epilogue),
+                                            None if bias is None else bias.data_ptr(), workspace.data_ptr(),
+                                            workspace.numel(), _dt(x), _stream(x.device))
+        _lib.check(code, "cram_gemm_splitk")
+    else:
+        code = _lib.load().cram_gemm_splitk_residual(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0),
+                                                     r2.data_ptr(), r2.stride(0), o2.data_ptr(), o2.stride(0), M, N, K,
+                                                     int(splits), workspace.data_ptr(), workspace.numel(), _dt(x),
+                                                     _stream(x.device))
+        _lib.check(code, "cram_gemm_splitk_residual")
     if ev is not None:
         ev.record(torch.cuda.current_stream(x.device))
     return out

@@ -50,7 +50,7 @@ extern "C" {
 
 #define CRAM_ABI_VERSION 5        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
                                      4: cram_get_knob(which, *value), decode projection GEMM;
-                                     5: cram_gemm_residual, cram_gemm_rope */
+                                     5: cram_gemm_residual, cram_gemm_rope, cram_gemm_splitk_residual */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -242,6 +242,16 @@ size_t cram_gemm_splitk_workspace_size(int M, int N, int splits);
 int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N,
                      int K, int splits, int epilogue, const void* bias, void* workspace, size_t ws_bytes, int dtype,
                      cram_stream_t stream);
+
+/*
+ * Split-K with cram_gemm_residual's epilogue: out = rnd(res + rnd(sum)) (res may be out itself).  The engine runs the
+ * sparse last wave of the sweep's o_proj / down_proj tiles through it (rows past the last whole wave of 256 x 256
+ * tiles on the 256 CUs, cut into K ranges so they fill the chip) instead of leaving most CUs idle for one tile time.
+ * Requirements of cram_gemm_splitk plus those of cram_gemm_residual on res / ldr.
+ */
+int cram_gemm_splitk_residual(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* res, int64_t ldr,
+                              void* out, int64_t ldo, int M, int N, int K, int splits, void* workspace,
+                              size_t ws_bytes, int dtype, cram_stream_t stream);
 
 /*
  * Host-side prompt -> credibility weights (cram_spans.cpp; no device, no stream), batched over B prompts.

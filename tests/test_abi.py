@@ -88,6 +88,16 @@ def test_argument_validation_without_gpu():
     assert rope(dtype=1) == -2
     assert rope(K=64) == -2
     assert rope(ldo=6148) == -3
+    # split-K residual: residual checks, then split-K's (workspace)
+    ws4 = L.cram_gemm_splitk_workspace_size(16, 512, 4)
+    assert L.cram_gemm_splitk_residual(fake, 512, fake, 512, None, 512, fake, 512, 16, 512, 512, 4, fake, ws4, 0,
+                                       None) == -1
+    assert L.cram_gemm_splitk_residual(fake, 512, fake, 512, far, 516, fake, 512, 16, 512, 512, 4, fake, ws4, 0,
+                                       None) == -3
+    assert L.cram_gemm_splitk_residual(fake, 512, fake, 512, fake + 1024, 512, fake, 512, 16, 512, 512, 4, fake, ws4,
+                                       0, None) == -1
+    assert L.cram_gemm_splitk_residual(fake, 512, fake, 512, far, 512, fake, 512, 16, 512, 512, 4, None, ws4, 0,
+                                       None) == -5
     # split-K GEMM: K % (64 * splits), epilogue, bias only with STORE, workspace presence and size
     ws = L.cram_gemm_splitk_workspace_size(16, 512, 4)
     assert ws == 4 * 16 * 512 * 4

@@ -374,3 +374,44 @@ def test_engine_fused_qkv_layer_matches_library_path(gpu_device):
         d = (of.float() - ol.float()).abs()
         scale = ol.float().abs().mean().item()
         assert d.max().item() <= 0.05 * ol.float().abs().max().item() and d.mean().item() <= 0.01 * scale
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(512, 4096, 4096, 8), (77, 512, 14336, 4), (256, 768, 1024, 2)])
+def test_gemm_splitk_residual(gpu_device, M, N, K, splits):
+    """cram_gemm_splitk_residual: rnd(res + rnd(sum over the K ranges)), bit-identical to split-K STORE followed by a
+    model-dtype add, in place too."""
+    x, w = _operands(M, N, K, torch.bfloat16, gpu_device, 19 * M + K)
+    res = (torch.randn(M, N, generator=torch.Generator().manual_seed(M)) * 2).to(torch.bfloat16).to(gpu_device)
+    out = ops.gemm_splitk(x, w, splits, residual=res)
+    exp = ops.gemm_splitk(x, w, splits) + res
+    inplace = res.clone()
+    ops.gemm_splitk(x, w, splits, residual=inplace, out=inplace)
+    torch.cuda.synchronize()
+    assert torch.equal(out, exp) and torch.equal(inplace, out)
+
+
+@pytest.mark.parametrize("K", [4096, 14336])
+def test_engine_residual_gemm_tail_split(gpu_device, K):
+    """CrAMEngine._gemm_residual at the sweep's row count M = 29,184 (N = 4096: 1,824 tiles = 7 waves of 256 + 32):
+    rows past the last whole wave go through split-K.  Rows in the whole waves are bit-identical to the one-launch
+    residual GEMM, tail rows to split-K + add; all within the final-rounding bar of the float32 product."""
+    from cram_amd import engine as E
+    sp = E.ModelSpec(1, 1024, 8, 2, 128, 1536, 1000, 1e-5, False)
+    eng = E.CrAMEngine.random(sp, gpu_device, seed=3, std=0.03)
+    M, N = 29184, 4096
+    x, w = _operands(M, N, K, torch.bfloat16, gpu_device, 23 + K)
+    h = (torch.randn(M, N, generator=torch.Generator().manual_seed(9)) * 2).to(torch.bfloat16).to(gpu_device)
+    out = eng._gemm_residual(x, w, h)
+    one = ops.gemm(x, w, residual=h)
+    Mm = 28672                                    # 7 waves x 256 tiles / 16 column tiles = 112 row tiles
+    torch.cuda.synchronize()
+    assert torch.equal(out[:Mm], one[:Mm])
+    assert not torch.equal(out[Mm:], one[Mm:])    # the tail did go through the other kernel
+    for s in (8,):
+        assert torch.equal(out[Mm:], ops.gemm_splitk(x[Mm:], w, s) + h[Mm:])
+    rows = slice(Mm - 64, M)
+    ref = x[rows].float() @ w.float().t()
+    acc_tol = 2.0 ** -22 * (x[rows].float().abs() @ w.float().abs().t())
+    d = (out[rows].float() - (ref + h[rows].float())).abs()
+    bar = _ulp(ref, torch.bfloat16) + _ulp(ref + h[rows].float(), torch.bfloat16) + acc_tol
+    assert (d <= bar).all(), float(d.max())
