@@ -95,10 +95,10 @@ PREFILL_CHUNK_ROWS = 32768
 
 
 def padded_rows(M: int, spec: Optional["ModelSpec"] = None) -> int:
-    """GEMM row count for M rows: rounded up to the 256-row macro tile (measured: M % 256 == 0 is ~4% faster) and,
-    for the Llama-3-8B projection shapes, to the row count within +2048 that minimises the measured per-layer GEMM
-    time plus the per-row elementwise work (data/gemm_rows.json: rows that fill whole waves of 256x256 tiles on the
-    256 CUs run 3-7 % cheaper per row)."""
+    """GEMM row count for M rows: rounded up to the 256-row macro tile and, for the Llama-3-8B projection shapes, to
+    the row count within +2048 that minimises the measured per-layer GEMM time plus the per-row non-GEMM work
+    (data/gemm_rows.json, the engine's own fused GEMMs with the residual tail split: ~311-314 ns per row at most
+    row counts, 307-309 at multiples of 4096; round 3's hipBLASLt table had 290 vs 305-315)."""
     Mp = -(-M // ROW_ALIGN) * ROW_ALIGN
     tab = _row_table(spec)
     if tab is None or Mp not in tab:
@@ -107,9 +107,9 @@ def padded_rows(M: int, spec: Optional["ModelSpec"] = None) -> int:
     return min(cands, key=lambda m: (tab[m] + ROW_COST_MS * m, m))
 
 
-# elementwise work per GEMM row of a suffix layer (RMSNorm, SiLU-mul, RoPE, copies: ~9.5 % of the sweep step
-# against the GEMMs' 87 %, i.e. ~33 ns per row next to ~300 ns of GEMM)
-ROW_COST_MS = 33e-6
+# non-GEMM work per GEMM row of a suffix layer (attention, RMSNorm, copies: ~5.7 % of the sweep step against the fused
+# GEMMs' 94 % in round 4's rocprof summary, i.e. ~19 ns per row next to ~311 ns of GEMM)
+ROW_COST_MS = 19e-6
 _ROW_TABLES = {}
 
 
