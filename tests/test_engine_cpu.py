@@ -381,4 +381,4 @@ def test_padded_rows_table():
         assert p % 256 == 0 and M <= p <= -(-M // 256) * 256 + 2048
         assert padded_rows(M) == -(-M // 256) * 256
         assert padded_rows(M, ModelSpec.qwen2_7b()) == padded_rows(M)
-    assert padded_rows(28050, sp) == 28672        # measured: 28672 rows (7 x 4096) run cheaper than 28160
+    assert padded_rows(32400, sp) == 32768        # measured: 32768 rows (8 x 4096) run cheaper than 32512
