@@ -264,8 +264,9 @@ class CrAMEngine:
             return self._gemm_residual(act, lw.wd, h), None
         return h, self.mlp(x, lw)
 
-    # gate/up with the fused activation: bf16 (the 4-wave kernel's type), 256-row tiles filled, the weight interleaved
-    FUSED_MLP_MIN_ROWS = 4096
+    # the fused GEMMs from one full 256-row tile: every sweep / packed-prefill call, and the sweep's baseline forward
+    # (T ~ 1k rows, 0.2 % of the sweep's FLOPs) so no separate RoPE / SiLU-mul pass is left in the sweep
+    FUSED_MLP_MIN_ROWS = 256
 
     def _fused_mlp_ok(self, x: torch.Tensor) -> bool:
         if not FUSED_MLP or self.device.type != "cuda" or self.dtype != torch.bfloat16:
@@ -327,8 +328,11 @@ class CrAMEngine:
     def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin, pos: Optional[torch.Tensor] = None):
         """x [B, T, D] -> roped q [B, T, Hq, d], k / v [B, T, Hkv, d]: strided views of one fused buffer."""
         sp = self.spec
-        y = ops.linear(x, lw.wqkv, lw.bqkv)
-        ops.rope_inplace(y, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=y.shape[-2], pos=pos)
+        if self._fused_qkv_ok(x, lw) and x.is_contiguous():
+            y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T=x.shape[-2], pos=pos)
+        else:
+            y = ops.linear(x, lw.wqkv, lw.bqkv)
+            ops.rope_inplace(y, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=y.shape[-2], pos=pos)
         q = y[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
         k = y[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
         v = y[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
