@@ -139,6 +139,16 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def gemm_source_hash() -> str:
+    """Identity of the projection GEMM's source (cram_gemm.hip, the generated K loop, the ABI header): the GEMM PMC
+    evidence (profiles/gemm_pmc.json) records it, and bench.py applies that evidence only while it matches."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in (CSRC / "cram_gemm.hip", CSRC / "gemm_w4_loop.inc", REPO_DIR / "include" / "cram_attn.h"):
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def x64_asm_path() -> Path:
     """Device assembly of cram_attn.hip saved by the last build (-save-temps=obj)."""
     return asm_path("cram_attn.hip")

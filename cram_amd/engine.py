@@ -533,8 +533,12 @@ def decode_splits(N: int, K: int, rows: int) -> int:
 
 def decode_attn_splits(B: int, num_kv_heads: int, S_max: int) -> int:
     """Split-S count of the decode attention: enough (batch row, kv head) work items x splits to cover ~512
-    workgroups, at most 16 splits and at least 256 keys per split."""
+    workgroups, at most 16 splits and at least 256 keys per split; long rows (>= 4096 keys) take at least 2 while
+    there are fewer than 2048 work items (config 5, B = 129 x 8 kv heads, 8.4k keys: 5.54 -> 5.77 TB/s;
+    B = 512 x 1k keys stays at 1 split: 2 measured 0.91x; tools/prof_decode.py, profiles/r04/dsplit/)."""
     splits = max(1, min(16, math.ceil(512 / max(1, B * num_kv_heads))))
+    if S_max >= 4096 and B * num_kv_heads < 2048:
+        splits = max(splits, 2)
     return max(1, min(splits, S_max // 256))
 
 

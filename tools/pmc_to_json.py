@@ -1,4 +1,5 @@
-"""rocprofv3 PMC passes of the IE-sweep attention launch -> profiles/attn_pmc.json.
+"""rocprofv3 PMC passes of the IE-sweep attention launch -> profiles/attn_pmc.json, or (--gemm) of the sweep's
+dominant GEMM launch (gemm_w4_kernel, gate/up + SiLU-mul at M = 29,184; tools/pmc_gemm.sh) -> profiles/gemm_pmc.json.
 
 Input: the directory tools/pmc_attn.sh wrote (p1..p5/p*_counter_collection.csv, one --pmc pass each, kernel-trace
 only), or a directory holding them further down.  Output: what the north star asks rocprof to report for the
@@ -25,13 +26,17 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-from cram_amd.build import kernel_source_hash  # noqa: E402
+from cram_amd.build import gemm_source_hash, kernel_source_hash  # noqa: E402
 from cram_amd.ops import prefill_work  # noqa: E402
 
+GEMM = "--gemm" in sys.argv
+ARGS = [a for a in sys.argv[1:] if a != "--gemm"]
 B, T, Hq, Hkv, d = 33, 962, 32, 8, 128          # tools/prof_attn.py's default: the IE sweep's attention launch
+GM, GN, GK = 29184, 28672, 4096                  # tools/gemm_pmc.py: gate/up (+ SiLU-mul, output N / 2 wide)
 SIMDS = 1024                                     # 256 CUs x 4 SIMDs
 XCDS = 8
-MFMA_FLOP = 32 * 32 * 16 * 2                     # v_mfma_f32_32x32x16_bf16
+# FLOP per MFMA instruction: v_mfma_f32_32x32x16_bf16 (attention) / v_mfma_f32_16x16x32_bf16 (GEMM)
+MFMA_FLOP = 16 * 16 * 32 * 2 if GEMM else 32 * 32 * 16 * 2
 PEAK_TFLOPS, PEAK_GBS = 2500.0, 8000.0           # dense bf16 MFMA, HBM3E (MI355X_MICROARCH.md chip table)
 
 
@@ -55,10 +60,13 @@ def mean(rows, what=0):
 
 
 def main():
-    src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-    dst = sys.argv[2] if len(sys.argv) > 2 else os.path.join(REPO, "profiles", "attn_pmc.json")
+    src = ARGS[0] if ARGS else ("gpurun_out/gemm_pmc" if GEMM else "gpurun_out/pmc")
+    dst = ARGS[1] if len(ARGS) > 1 else os.path.join(REPO, "profiles", "gemm_pmc.json" if GEMM else "attn_pmc.json")
     c, kernels = load(src)
-    flops, alg_bytes = prefill_work(B, Hq, Hkv, T, T, d, 0)
+    if GEMM:
+        flops, alg_bytes = 2.0 * GM * GN * GK, 2.0 * (GM * GK + GN * GK + GM * GN // 2)
+    else:
+        flops, alg_bytes = prefill_work(B, Hq, Hkv, T, T, d, 0)
     read_b = mean(c["FETCH_SIZE"]) * 1024 * 2
     write_b = mean(c["WRITE_SIZE"]) * 1024
     traffic = read_b + write_b
@@ -72,7 +80,8 @@ def main():
     n_mfma = mean(c["SQ_INSTS_MFMA"])
     out = {
         "kernel": " / ".join(sorted(kernels)),
-        "shape": {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d},
+        "shape": ({"M": GM, "N": GN, "K": GK, "epilogue": "SiLU-mul"} if GEMM else
+                  {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d}),
         "dispatches": len(c["FETCH_SIZE"]),
         "fetch_size_kib": mean(c["FETCH_SIZE"]), "write_size_kib": mean(c["WRITE_SIZE"]),
         "hbm_read_bytes": read_b, "hbm_write_bytes": write_b, "hbm_bytes_per_launch": traffic,
@@ -89,11 +98,12 @@ def main():
         "wait_any_frac": round(mean(c["SQ_WAIT_ANY"]) / mean(c["SQ_WAVE_CYCLES"]), 4),
         "lds_bank_conflict_per_lds_inst": round(mean(c["SQ_LDS_BANK_CONFLICT"]) / mean(c["SQ_INSTS_LDS"]), 4),
         "source": os.path.relpath(os.path.abspath(src), REPO),
-        "kernel_source_hash": kernel_source_hash(),
-        "note": ("rocprofv3 --pmc in separate passes (tools/pmc_attn.sh). traffic: FETCH_SIZE x2 (gfx950 16 B/lane "
+        "kernel_source_hash": gemm_source_hash() if GEMM else kernel_source_hash(),
+        "note": (f"rocprofv3 --pmc in separate passes (tools/{'pmc_gemm' if GEMM else 'pmc_attn'}.sh). traffic: "
+                 "FETCH_SIZE x2 (gfx950 16 B/lane "
                  "read undercount) + WRITE_SIZE, KiB -> B; hbm_gbs / tflops: over the dispatches' own wall time; "
                  "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); effective clock = "
-                 "GRBM_GUI_ACTIVE / 8 / wall; mfma issues x 32768 FLOP / algorithmic FLOPs"),
+                 f"GRBM_GUI_ACTIVE / 8 / wall; mfma issues x {MFMA_FLOP} FLOP / algorithmic FLOPs"),
     }
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
