@@ -12,7 +12,10 @@ L = int(sys.argv[2]) if len(sys.argv) > 2 else 32
 path = sorted(glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True))[0]
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
 is_att = lambda name: "decode_mfma_kernel" in name or "decode_kernel<" in name or "decode_kernelI" in name
-first = next(i for i, r in enumerate(rows) if is_att(r["Kernel_Name"]))
+# the packed prefill's last layer also runs the decode attention (one call per chunk) and its projections run on
+# gemm_w4_kernel, which the steps never use: the steps start at the first decode attention after the last w4 dispatch
+last_w4 = max([i for i, r in enumerate(rows) if "gemm_w4_kernel" in r["Kernel_Name"]], default=-1)
+first = next(i for i, r in enumerate(rows) if i > last_w4 and is_att(r["Kernel_Name"]))
 steps_rows = rows[first:]
 n_att = sum(1 for r in steps_rows if is_att(r["Kernel_Name"]))
 n_steps = max(1, n_att // L)
