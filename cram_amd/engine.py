@@ -88,10 +88,6 @@ FUSED_RESIDUAL = os.environ.get("CRAM_FUSED_RESIDUAL", "1") != "0"
 # q/k/v projection with RoPE in cram_gemm's epilogue (bf16, head_dim 128, no q/k/v bias) at the same row counts;
 # CRAM_FUSED_QKV=0: hipBLASLt + cram_rope_inplace / cram_rope_split (A/B)
 FUSED_QKV = os.environ.get("CRAM_FUSED_QKV", "1") != "0"
-# decode steps of >= 2 x DECODE_STREAMS_MIN_ROWS rows as two half-batch graphs on two streams (CrAMEngine.generate);
-# CRAM_DECODE_STREAMS=1: one graph over the whole batch (A/B)
-DECODE_STREAMS = int(os.environ.get("CRAM_DECODE_STREAMS", "2"))
-DECODE_STREAMS_MIN_ROWS = 128
 # the sparse last wave of the residual GEMMs' tiles through split-K (CrAMEngine._gemm_residual); 0 = one launch (A/B)
 TAIL_SPLIT = os.environ.get("CRAM_TAIL_SPLIT", "1") != "0"
 # packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where hipBLASLt already runs at full rate
@@ -466,63 +462,34 @@ class CrAMEngine:
         if ev is not None:
             phases["t0"] = ev()
             phases["t0"].record()
-        B = len(prompts)
-        steps = max_new_tokens - 1
-        # two half-batch sessions whose graphs replay on two streams: one half's decode attention (HBM-bound) runs
-        # beside the other half's projections (matrix cores); rows are independent, so the ids are unchanged
-        # (rows dealt alternately, so two halves of a length-sorted batch carry equal K/V)
-        groups = [list(range(B))]
-        if DECODE_STREAMS == 2 and use_graph and steps > 0 and B >= 2 * DECODE_STREAMS_MIN_ROWS:
-            groups = [list(range(0, B, 2)), list(range(1, B, 2))]
-        sessions = [DecodeSession(self, [prompts[i] for i in g], [weights16[i] for i in g], layers_to_heads,
-                                  max_new_tokens, bad_token_ids, repetition_penalty) for g in groups]
-        for sess in sessions:
-            sess.prefill()
+        sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids,
+                             repetition_penalty)
+        sess.prefill()
         if ev is not None:
             phases["prefill"] = ev()
             phases["prefill"].record()
+        steps = max_new_tokens - 1
         if use_graph and steps > 0:
-            for sess in sessions:
-                sess.capture()
+            sess.capture()
         if ev is not None:
             phases["capture"] = ev()
             phases["capture"].record()
         eos = torch.tensor(list(eos_ids) or [-1], device=self.device)
-        main = torch.cuda.current_stream(self.device)
-        side = None
-        if len(sessions) > 1:
-            side = [torch.cuda.Stream(self.device) for _ in sessions]
-            for st in side:
-                st.wait_stream(main)
         n_steps = 0
         for t in range(steps):
-            if side is None:
-                sessions[0].step(use_graph)
-            else:
-                for sess, st in zip(sessions, side):
-                    with torch.cuda.stream(st):
-                        sess.step(use_graph)
+            sess.step(use_graph)
             n_steps += 1
             # every 8 steps: stop once every row has produced an EOS (one host sync per check)
             if stop_on_eos and eos_ids and (t % 8 == 7 or t == steps - 1):
-                if side is not None:
-                    for st in side:
-                        main.wait_stream(st)
-                if all(bool(torch.isin(sess.generated(), eos).any(1).all()) for sess in sessions):
+                if bool(torch.isin(sess.generated(), eos).any(1).all()):
                     break
-        if side is not None:
-            for st in side:
-                main.wait_stream(st)
         if ev is not None:
             phases["steps"] = ev()
             phases["steps"].record()
             phases["n_steps"] = n_steps
-            phases["lens"] = [n for sess in sessions for n in sess.lens]
+            phases["lens"] = list(sess.lens)
         out = []
-        gen = [None] * B
-        for g, sess in zip(groups, sessions):
-            for i, row in zip(g, sess.generated().cpu().tolist()):
-                gen[i] = row
+        gen = sess.generated().cpu().tolist()
         for row in gen:
             row = row[:max_new_tokens]
             if eos_ids:

@@ -189,31 +189,6 @@ def test_engine_batched_decode_matches_dropin(paths, nq, gpu_device):
                 break
 
 
-def test_engine_two_stream_decode_equals_its_halves(paths, nq, gpu_device):
-    """generate() over >= 256 rows runs two half-batch step graphs on two streams (rows dealt alternately): the ids
-    are exactly those of the two halves decoded one after the other, each as one graph."""
-    from cram_amd import engine as E
-    heads = {0: [1], 1: [0, 3], 3: [2]}
-    obj = _drop_in(paths, "llama3", heads, gpu_device)
-    prompts, ws = [], []
-    for i in range(260):
-        rec = nq[i % 40]
-        sc = [0.1, 1, 1, 1, 1] if i % 3 else [1, 1, 0.1, 1, 1]
-        enc, w = obj.decode_with_special_attention(question=rec["question"],
-                                                   paras=rec["ori_fake"] + rec["reranked_dense_ctxs"], scores=sc)
-        prompts.append(enc["input_ids"][0])
-        ws.append(w.cpu())
-    assert E.DECODE_STREAMS == 2 and len(prompts) >= 2 * E.DECODE_STREAMS_MIN_ROWS
-    both = obj.engine.generate(prompts, ws, heads, max_new_tokens=16)
-    prev = E.DECODE_STREAMS
-    E.DECODE_STREAMS = 1
-    try:
-        halves = [obj.engine.generate(prompts[k::2], ws[k::2], heads, max_new_tokens=16) for k in (0, 1)]
-    finally:
-        E.DECODE_STREAMS = prev
-    assert both[0::2] == halves[0] and both[1::2] == halves[1]
-
-
 def test_engine_repetition_penalty_matches_dropin(paths, nq, gpu_device):
     """Qwen chat checkpoints ship generation_config.repetition_penalty = 1.05, which model.generate applies in
     greedy decoding: run_RAG_batch (engine, graph-replayed) must apply it too.  The tiny Qwen2's config is set to
