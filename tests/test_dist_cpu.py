@@ -136,6 +136,8 @@ def _worker(rank, world, port, root, out_path, shard_dir, die_after):
     from cram_amd.engine import CrAMEngine
     from tests import cpu_ops
     from tests import tiny_models as tm
+    torch.distributed.init_process_group("gloo", init_method=f"file://{out_path}.{port}.store", rank=rank,
+                                         world_size=world)             # file rendezvous: no port race under xdist
     r, w, _ = cdist.init("gloo")
     assert (r, w) == (rank, world)
     path = os.path.join(root, tm.DIR_NAME[KIND])
@@ -254,6 +256,9 @@ def _dec_worker(rank, world, port, root, out_path, shard_dir, die_after):
     from cram_amd.engine import CrAMEngine
     from tests import cpu_ops
     from tests import tiny_models as tm
+    # rendezvous through a file next to the outputs (no TCP port to race for under pytest-xdist), then cdist.init
+    # reads rank / world from the torch.distributed.run environment as under the launcher
+    torch.distributed.init_process_group("gloo", init_method=f"file://{out_path}.{port}.store", rank=rank, world_size=world)
     cdist.init("gloo")
     path = os.path.join(root, tm.DIR_NAME[KIND])
     eng = CrAMEngine.from_hf(AutoModelForCausalLM.from_pretrained(path, dtype="auto").eval())
