@@ -510,6 +510,7 @@ class CrAMEngine:
 DECODE_GEMM_MAX_ROWS = 512
 DECODE_GEMM_TARGET_WGS = 128
 DECODE_GEMM_MIN_K_OVER_N = 2
+DECODE_QKV_SPLIT_MAX_ROWS = 192
 
 
 def decode_splits(N: int, K: int, rows: int) -> int:
@@ -588,6 +589,14 @@ class DecodeSession:
         D, F, qkv = sp.hidden, sp.intermediate, sp.q_size + 2 * sp.kv_size
         self.splits_gemm = {"qkv": decode_splits(qkv, D, self.B), "o": decode_splits(D, sp.q_size, self.B),
                             "gu": decode_splits(2 * F, D, self.B), "down": decode_splits(D, F, self.B)}
+        if not self.splits_gemm["qkv"] and self.B <= DECODE_QKV_SPLIT_MAX_ROWS and os.environ.get("CRAM_DECODE_GEMM",
+                                                                                                   "1") != "0":
+            # one partly filled row tile (config 5: 129 rows): q/k/v over 8 K ranges, 28 vs 41 us on hipBLASLt's pick
+            # (Llama-3, tools/decode_gemm_probe.py --M 129, profiles/r04/dec129/); o_proj / gate/up stay on the library
+            self.splits_gemm["qkv"] = 8 if D % (64 * 8) == 0 and qkv % 256 == 0 else 0
+        # lm_head on the 4-wave kernel (bf16, vocab % 256 == 0): 225 vs 290 us at 129 rows, 418 vs 457 at 512
+        self.lm_w4 = (eng.dtype == torch.bfloat16 and eng.lm_head.shape[0] % 256 == 0 and D % 64 == 0 and D >= 128
+                      and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         shapes = {"qkv": qkv, "o": D, "gu": 2 * F, "down": D}
         need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in self.splits_gemm.items() if v]
                    or [0])
@@ -722,7 +731,7 @@ class DecodeSession:
             h, x2 = eng.add_rmsnorm(self._proj(a.flatten(-2)[:, None], lw.wo, None, "o"), h, lw.ln2)
             m = self._mlp(x2, lw)
         _, hn = eng.add_rmsnorm(m[:, 0], h[:, 0], eng.norm)
-        nxt = self._pick(ops.linear(hn, eng.lm_head))
+        nxt = self._pick(ops.gemm(hn, eng.lm_head, name="gemm") if self.lm_w4 else ops.linear(hn, eng.lm_head))
         self.tokens.copy_(nxt)
         self.out.index_copy_(1, self.t.view(1), nxt[:, None])
         self.t.add_(1)
