@@ -64,7 +64,8 @@ def test_config4_shape_selects_the_gqa7_kernels(qwen7):
 @pytest.mark.parametrize("decode_gemm", ["rule", "all"])
 def test_config4_engine_decode_matches_dropin(qwen7, decode_gemm, monkeypatch):
     """run_RAG_batch (engine: packed varlen prefill, graph-replayed steps, split-K decode projections — by the
-    engine's rule, or all of them including the biased q/k/v with CRAM_DECODE_GEMM=all) == the transformers
+    engine's rule (down_proj; the biased q/k/v too at these few rows), or all of them with CRAM_DECODE_GEMM=all),
+    lm_head on the 4-wave GEMM == the transformers
     drop-in's model.generate on the cram_hip kernels, up to the first near-tie."""
     from cram_amd import attention as A
     from cram_amd.engine import DecodeSession
@@ -73,7 +74,9 @@ def test_config4_engine_decode_matches_dropin(qwen7, decode_gemm, monkeypatch):
     obj, _, recs = qwen7
     sk = DecodeSession(obj.engine, [torch.zeros(900, dtype=torch.long)] * 2, [torch.ones(1, 900, dtype=torch.float16)] * 2,
                        {}, 4).splits_gemm
-    assert (sk["qkv"] > 0) == (decode_gemm == "all") and sk["down"] > 0, sk
+    # the rule: down_proj (long K) always; q/k/v at <= 192 rows (one partly filled row tile); o_proj / gate/up only
+    # with CRAM_DECODE_GEMM=all
+    assert sk["qkv"] > 0 and sk["down"] > 0 and (sk["o"] > 0) == (sk["gu"] > 0) == (decode_gemm == "all"), sk
     heads = obj.layers_to_be_modified
     qs, ps, ss = [r[0]["question"] for r in recs], [r[1] for r in recs], [r[2] for r in recs]
     batched = obj.run_RAG_batch(qs, ps, ss, max_new_tokens=16, use_graph=True)
