@@ -101,8 +101,8 @@ def test_gpt2_small_decode_all_heads(gpu_device, decode_variant, S):
 def test_config5_decode_long_context(gpu_device, decode_variant, B):
     """Config 5 decode step: B sequences of 8,150-8,400 cached keys (ragged), GQA 32/8, 20 passage spans per prompt
     (a -inf span, log-0.1 spans, 1.0 elsewhere), top-half heads re-weighted, the engine's split count: B = 143 is the
-    bench's batch (the rows the KV budget holds: 0.55 x 288 GB / 1.1 GB per row; 2 splits since round 4), B = 16 the round-3 batch
-    (4 splits).  Every row vs float64 at B = 16, 8 sampled rows at B = 143."""
+    bench's batch (the rows the KV budget holds: 0.55 x 288 GB / 1.1 GB per row; 2 splits since round 4), B = 16
+    the round-3 batch (4 splits).  Every row vs float64 at B = 16, 8 sampled rows at B = 143."""
     from cram_amd import ops
     from cram_amd.engine import decode_attn_splits
     dev = gpu_device
