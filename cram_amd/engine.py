@@ -524,10 +524,13 @@ def decode_splits(N: int, K: int, rows: int) -> int:
         return 0
     tiles = N // 256          # column tiles; the row tiles (rows > 256) are not counted: 8 ranges won at both 256 and
     best = 0                  # 512 rows (profiles/r03/s5_m512/probe_*.jsonl: Llama-3 down 67 vs 93 us at 4 ranges)
+    # at <= 192 rows more ranges pay: Llama-3 down at 129 rows 41.9 us at 14 ranges (224 workgroups) vs 48.0 at 8
+    # (profiles/r04/dec129/)
+    target = DECODE_GEMM_TARGET_WGS if rows > DECODE_QKV_SPLIT_MAX_ROWS else 224
     for s in range(1, K // 256 + 1):
         if K % (64 * s):
             continue
-        if not best or abs(tiles * s - DECODE_GEMM_TARGET_WGS) < abs(tiles * best - DECODE_GEMM_TARGET_WGS):
+        if not best or abs(tiles * s - target) < abs(tiles * best - target):
             best = s
     return best
 
@@ -595,8 +598,8 @@ class DecodeSession:
             # (Llama-3, tools/decode_gemm_probe.py --M 129, profiles/r04/dec129/); o_proj / gate/up stay on the library
             self.splits_gemm["qkv"] = 8 if D % (64 * 8) == 0 and qkv % 256 == 0 else 0
         # lm_head on the 4-wave kernel (bf16, vocab % 256 == 0): 225 vs 290 us at 129 rows, 418 vs 457 at 512
-        self.lm_w4 = (eng.dtype == torch.bfloat16 and eng.lm_head.shape[0] % 256 == 0 and D % 64 == 0 and D >= 128
-                      and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
+        self.lm_w4 = (eng.device.type == "cuda" and eng.dtype == torch.bfloat16 and eng.lm_head.shape[0] % 256 == 0
+                      and D % 64 == 0 and D >= 128 and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         shapes = {"qkv": qkv, "o": D, "gu": 2 * F, "down": D}
         need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in self.splits_gemm.items() if v]
                    or [0])
