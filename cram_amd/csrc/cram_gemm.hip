@@ -40,9 +40,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <algorithm>
-#include <cstdlib>
-#include <atomic>
 #include <type_traits>
 
 #include "../../include/cram_attn.h"
@@ -430,10 +427,20 @@ __device__ __forceinline__ int2 tile_of_w4(const GemmParams& p, int bid) {     /
 template <typename T, int EPI>
 __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(1024))) char smem[W4_LDS];
+  const int2 tt = tile_of_w4(p, blockIdx.x);
+  const int tm = tt.x, tn = tt.y;
+  const int n0 = tn * BN, m0 = tm * BM;
   const int kc = p.kts * BK;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wn = wave & 1, wm = wave >> 1;
+
+  const T* xb = static_cast<const T*>(p.x) + (int64_t)n0 * p.ldx;
+  const T* yb = static_cast<const T*>(p.y) + (int64_t)m0 * p.ldy;
+  const int yrows = min(BM, p.M - m0);
+  // rows live in the per-lane voffset (range-checked: a row at or past M reads zeros), the K-tile in soffset
+  u32x4 sx = w4_srd(xb, (uint32_t)((BN - 1) * p.ldx * 2 + kc * 2));
+  u32x4 sy = w4_srd(yb, (uint32_t)((yrows - 1) * p.ldy * 2 + kc * 2));
   // LDS-DMA piece i of this wave: image rows 32 i + 8 wave .. +7 (the 4 waves' i-th pieces cover 32 adjacent rows);
   // lane L fetches row + L / 8, chunk (L % 8) ^ swz(row)
   uint32_t vx[8], vy[8];
@@ -445,40 +452,14 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
     vy[i] = (uint32_t)(row * p.ldy * 2 + c * 16);
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
-  const uint32_t kend = (uint32_t)(p.kts * ROWB);
-  // fragment reads: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row fragment, k chunk 4 ks + g
-  const int fr = lane & 15, fg = lane >> 4;
-  // Persistent over output tiles t = blockIdx.x, + gridDim.x, ... (one workgroup per CU).  With an even K-tile count
-  // the stage the last two K-tiles leave free first (stage 0, free since B3 of tile kts - 2) receives the NEXT output
-  // tile's K-tile 0 before this tile's epilogue, which stages through stage 1 only: the next tile's first fetch
-  // overlaps this tile's epilogue instead of following it.
-#ifndef CRAM_W4_STAMPS
-  const bool warm_ok = (p.kts & 1) == 0;
-#else
-  const bool warm_ok = false;                    // the stamped diagnostic stream has no warm form
-#endif
-  bool warm = false;
-  for (int t = blockIdx.x; t < p.nblocks; t += gridDim.x) {
-  const int2 tt = tile_of_w4(p, t);
-  const int tm = tt.x, tn = tt.y;
-  const int n0 = tn * BN, m0 = tm * BM;
-  const T* xb = static_cast<const T*>(p.x) + (int64_t)n0 * p.ldx;
-  const T* yb = static_cast<const T*>(p.y) + (int64_t)m0 * p.ldy;
-  const int yrows = min(BM, p.M - m0);
-  // rows live in the per-lane voffset (range-checked: a row at or past M reads zeros), the K-tile in soffset
-  u32x4 sx = w4_srd(xb, (uint32_t)((BN - 1) * p.ldx * 2 + kc * 2));
-  u32x4 sy = w4_srd(yb, (uint32_t)((yrows - 1) * p.ldy * 2 + kc * 2));
-  // stage 0 destinations; the warm form enters with tile 0 already staged there (and the K offset at tile 1)
   uint32_t mx = __builtin_amdgcn_readfirstlane(lds0 + 1024 * wave);
   uint32_t my = __builtin_amdgcn_readfirstlane(lds0 + 32768 + 1024 * wave);
   // K offset of the next tile to stage (soffset); kend wraps it (the generated loop supports a rotated K start: a
   // staggered start per workgroup measured 0.97-0.99x, r04, so every workgroup starts at tile 0)
   uint32_t so = 0;
-  if (warm) {
-    mx ^= 0x10000u;
-    my ^= 0x10000u;
-    so = ROWB;
-  }
+  const uint32_t kend = (uint32_t)(p.kts * ROWB);
+  // fragment reads: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row fragment, k chunk 4 ks + g
+  const int fr = lane & 15, fg = lane >> 4;
   uint32_t rx0 = lds0 + (128 * wn + fr) * ROWB + ((fg ^ (fr >> 1)) * 16);
   uint32_t rx1 = lds0 + (128 * wn + fr) * ROWB + (((4 + fg) ^ (fr >> 1)) * 16);
   uint32_t ry0 = lds0 + 32768 + (128 * wm + fr) * ROWB + ((fg ^ (fr >> 1)) * 16);
@@ -499,13 +480,8 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
                  [vy6] "v"(vy[6]), [vy7] "v"(vy[7])                                                                  \
                : "memory", "scc", CRAM_V128_255_CLOBBERS, CRAM_A256_CLOBBERS)
 #ifndef CRAM_W4_STAMPS
-  if (warm) {
-    if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_W, "bf16");
-    else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_W, "f16");
-  } else {
-    if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "bf16");
-    else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "f16");
-  }
+  if constexpr (std::is_same<T, __bf16>::value) CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "bf16");
+  else CRAM_W4_ASM(CRAM_GEMM_W4_LOOP_A, "f16");
 #else
   // diagnostic build (tools/w4_stamps.hip): the stamped stream, its per-wave cycle sums (B1, B2, B3, whole tiles,
   // tile count) written to g_w4_stamps -- a buffer of its own, never an output element
@@ -527,70 +503,25 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
                : "memory", "scc", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91",
                  "s92", "s93", "s94", "s95", CRAM_V128_255_CLOBBERS, CRAM_A256_CLOBBERS);
   if (lane == 0) {
-    unsigned* o = g_w4_stamps + ((size_t)t * 4 + wave) * 5;
+    unsigned* o = g_w4_stamps + ((size_t)blockIdx.x * 4 + wave) * 5;
     o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st4;
   }
 #endif
 #undef CRAM_W4_ASM
 
-  // the next output tile's K-tile 0 into stage 0 (no wave reads stage 0 after B3 of K-tile kts - 2, which every
-  // wave has passed): 8 activation then 8 weight pieces, the prologue's order and m0 stepping
-  warm = warm_ok && t + (int)gridDim.x < p.nblocks;
-  if (warm) {
-    const int2 nt = tile_of_w4(p, t + gridDim.x);
-    const T* nxb = static_cast<const T*>(p.x) + (int64_t)(nt.y * BN) * p.ldx;
-    const T* nyb = static_cast<const T*>(p.y) + (int64_t)(nt.x * BM) * p.ldy;
-    const u32x4 nsx = w4_srd(nxb, (uint32_t)((BN - 1) * p.ldx * 2 + kc * 2));
-    const u32x4 nsy = w4_srd(nyb, (uint32_t)((min(BM, p.M - nt.x * BM) - 1) * p.ldy * 2 + kc * 2));
-    const uint32_t dx = __builtin_amdgcn_readfirstlane(lds0 + 1024 * wave);
-    const uint32_t dy = __builtin_amdgcn_readfirstlane(lds0 + 32768 + 1024 * wave);
-    uint32_t keep2;
-    asm volatile("s_mov_b32 %[keep], m0\n\t"
-                 "s_nop 4\n\t"
-                 "s_mov_b32 m0, %[dy]\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy0], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy1], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy2], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy3], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy4], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy5], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy6], %[sy], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vy7], %[sy], 0 offen lds\n\t"
-                 "s_mov_b32 m0, %[dx]\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx0], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx1], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx2], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx3], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx4], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx5], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx6], %[sx], 0 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %[vx7], %[sx], 0 offen lds\n\t"
-                 "s_mov_b32 m0, %[keep]"
-                 : [keep] "=&s"(keep2)
-                 : [sx] "s"(nsx), [sy] "s"(nsy), [dx] "s"(dx), [dy] "s"(dy), [vx0] "v"(vx[0]), [vx1] "v"(vx[1]),
-                   [vx2] "v"(vx[2]), [vx3] "v"(vx[3]), [vx4] "v"(vx[4]), [vx5] "v"(vx[5]), [vx6] "v"(vx[6]),
-                   [vx7] "v"(vx[7]), [vy0] "v"(vy[0]), [vy1] "v"(vy[1]), [vy2] "v"(vy[2]), [vy3] "v"(vy[3]),
-                   [vy4] "v"(vy[4]), [vy5] "v"(vy[5]), [vy6] "v"(vy[6]), [vy7] "v"(vy[7])
-                 : "memory");
-  }
-
   // epilogue through LDS (the output stage of the guide's T21: row-contiguous 16-byte stores instead of 64 scattered
   // 8-byte stores per lane -- the 8-byte form left each workgroup a long store-issue tail).  Lane (r, g) holds acc tile
-  // (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]; each wave rounds its rows into its own 16 KiB of stage 1 (stage 0
-  // may be receiving the next tile's K-tile 0), 64 rows of 256 B per pass (two passes) or all 128 rows of 128 B of
-  // SiLU-mul output in one, 8-byte units swizzled by row so a ds_write lane group spreads over the banks, then reads
-  // back whole 16-byte row pieces and stores them (EPI_RESIDUAL: plus the residual piece at the same place, a pass's
-  // 16 fetched before its staging so their latency hides behind it).
+  // (a, b) = out[m + 16 b + r][n + 16 a + 4 g .. +3]; each wave rounds its 128 rows (256 B each, or 128 B of SiLU-mul
+  // output) into its own 32 KiB of the (now idle) ring, 8-byte units swizzled by row so a ds_write lane group spreads
+  // over the banks, then reads back whole 16-byte row pieces and stores them (EPI_RESIDUAL: plus the residual piece
+  // at the same place, all 32 fetched before the staging so their latency hides behind it).
   using V4 = typename GVec<T>::x4;
   using V8 = typename GVec<T>::x8;
   constexpr bool ROWS = EPI != CRAM_GEMM_SILU_MUL;            // one staged row = 128 output columns
   constexpr int RB = ROWS ? 256 : 128;                         // staged bytes per row
   constexpr int LPR = RB / 16;                                 // read-back lanes per row: 16 | 8
   constexpr int RPI = 64 / LPR;                                // rows per read-back instruction: 4 | 8
-  constexpr int PR = ROWS ? 64 : 128;                          // rows per pass (16 KiB per wave)
-  constexpr int NPASS = 128 / PR;
-  constexpr int NRB = PR / RPI;                                // read-back instructions per pass: 16
-  constexpr int BPP = PR / 16;                                 // accumulator row blocks per pass
+  constexpr int NRB = 128 / RPI;                               // read-back instructions per wave
   const int cl = lane % LPR, rl = lane / LPR;
   const int64_t col0 = ROWS ? (int64_t)n0 + 128 * wn + 8 * cl : (int64_t)(n0 / 2) + 64 * wn + 8 * cl;
   const int mw = m0 + 128 * wm;                                // the wave's first output row
@@ -598,140 +529,134 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmParams p) {
   // vout (with keep_k the k and v heads also stay in out); without kout every head goes to out (q, k rotated)
   const int hidx = (n0 + 128 * wn) >> 7;
   const int kind = EPI != EPI_ROPE ? 0 : (hidx < p.hq ? 0 : (hidx < p.hq + p.hkv ? 1 : 2));
-  T* ob = static_cast<T*>(p.out);
-  char* const wl = smem + 65536 + wave * 16384;
-  auto swz = [](int row) { return RB == 256 ? (row & 7) << 2 : ((row >> 1) & 3) << 2; };   // unit XOR (bits 2..4)
-  __syncthreads();                               // every wave's last fragment reads of stage 1 are done
-  static_for<NPASS>([&](auto hi) {
-    constexpr int h = decltype(hi)::value;
-    const int mp = mw + PR * h;                  // the pass's first output row
-    V8 rv[EPI == EPI_RESIDUAL ? NRB : 1];
-    if constexpr (EPI == EPI_RESIDUAL) {
-      const T* rb = static_cast<const T*>(p.res);
+  V8 rv[EPI == EPI_RESIDUAL ? NRB : 1];
+  if constexpr (EPI == EPI_RESIDUAL) {
+    const T* rb = static_cast<const T*>(p.res);
 #pragma unroll
-      for (int j = 0; j < NRB; ++j) {
-        const int m = mp + RPI * j + rl;
-        if (m < p.M) rv[j] = *reinterpret_cast<const V8*>(rb + (int64_t)m * p.ldr + col0);
-      }
+    for (int j = 0; j < NRB; ++j) {
+      const int m = mw + RPI * j + rl;
+      if (m < p.M) rv[j] = *reinterpret_cast<const V8*>(rb + (int64_t)m * p.ldr + col0);
     }
-    static_for<BPP>([&](auto bi) {
-      constexpr int b = BPP * h + decltype(bi)::value;
-      const int ml = 16 * decltype(bi)::value + fr;             // the lane's row within the pass
-      const int sw = swz(ml);
-      if constexpr (ROWS) {
-        static_for<8>([&](auto ai) {
-          constexpr int a = decltype(ai)::value;
-          const f32x4 v = acc4<4 * (8 * a + b)>();
-          V4 o;
+  }
+  __syncthreads();                               // every wave's last fragment reads are done (no LDS-DMA is pending)
+  char* const wl = smem + wave * 32768;
+  auto swz = [](int row) { return RB == 256 ? (row & 7) << 2 : ((row >> 1) & 3) << 2; };   // unit XOR (bits 2..4)
+  static_for<8>([&](auto bi) {
+    constexpr int b = decltype(bi)::value;
+    const int ml = 16 * b + fr;                  // the lane's row within the wave's 128
+    const int sw = swz(ml);
+    if constexpr (ROWS) {
+      static_for<8>([&](auto ai) {
+        constexpr int a = decltype(ai)::value;
+        const f32x4 v = acc4<4 * (8 * a + b)>();
+        V4 o;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = (T)v[i];
-          *reinterpret_cast<V4*>(wl + ml * RB + (((4 * a + fg) ^ sw) * 8)) = o;
-        });
-      } else {
-        // gate tiles a = 0, 1, 4, 5 and their up tiles a + 2 (weight rows interleaved in blocks of 32): the wave's
-        // output columns are f = 32 (a >> 2) + 16 (a & 1) + 4 g + i of its 64
-        static_for<4>([&](auto ji) {
-          constexpr int a = (decltype(ji)::value & 1) + 4 * (decltype(ji)::value >> 1);
-          const f32x4 gv = acc4<4 * (8 * a + b)>(), uv = acc4<4 * (8 * (a + 2) + b)>();
-          V4 o;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float g = rnd<T>(gv[i]), u = rnd<T>(uv[i]);
-            o[i] = (T)(rnd<T>(g / (1.0f + expf(-g))) * u);
-          }
-          const int unit = 8 * (a >> 2) + 4 * (a & 1) + fg;
-          *reinterpret_cast<V4*>(wl + ml * RB + ((unit ^ sw) * 8)) = o;
-        });
-      }
-    });
-    // each wave reads back only its own rows: its writes are ordered before its reads (no barrier needed)
-    if constexpr (EPI == EPI_RESIDUAL) {
-#pragma unroll
-      for (int j = 0; j < NRB; ++j) {            // fully unrolled: rv stays in registers
-        const int ml = RPI * j + rl;
-        V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (T)((float)rv[j][i] + (float)v[i]);
-        if (mp + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mp + ml) * p.ldo + col0) = v;
-      }
-    } else if constexpr (EPI == EPI_ROPE) {
-      // read-back by rotation pairs: 8 lanes per row, lane c holds columns 8c.. and 64 + 8c.. of the wave's head;
-      // rope_kernel's arithmetic on the staged (rounded) projection, x1' = rnd(rnd(x1 c1) + rnd(-x2 s1)),
-      // x2' = rnd(rnd(x2 c2) + rnd(x1 s2)), table row pos[m] (or pos0 + m % T).  Rows go in groups of 4
-      // instructions whose table / index loads are all issued before the group's first use (one wait per group).
-      const bool rot = kind < 2;
-      const bool split = p.kout != nullptr;
-      const bool to_out = !split || kind == 0 || p.keep_k;      // keep_k: the k / v heads stay in out too
-      const bool to_kv = split && kind != 0;
-      const int c8 = lane & 7, r8 = lane >> 3;
-      T* const kvb = static_cast<T*>(kind == 2 ? p.vout : p.kout) +
-                     (int64_t)(hidx - p.hq - (kind == 2 ? p.hkv : 0)) * p.kv_hs + 8 * c8;
-      const int64_t colw = (int64_t)n0 + 128 * wn + 8 * c8;
-      const T* const cosb = static_cast<const T*>(p.cos_t) + 8 * c8;
-      const T* const sinb = static_cast<const T*>(p.sin_t) + 8 * c8;
-#pragma unroll 1
-      for (int g = 0; g < PR / 32; ++g) {
-        int64_t tp[4], kd[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int m = mp + 8 * (4 * g + u) + r8;
-          const bool live = m < p.rows;
-          tp[u] = !live ? 0 : (p.pos ? p.pos[m] : p.pos0 + (int64_t)(m % p.T));
-          kd[u] = 0;
-          if (to_kv && live) {
-            const int64_t sb = p.dst_b ? p.dst_b[m] : (int64_t)(m / p.T);
-            const int64_t t_ = p.dst_b ? tp[u] : (int64_t)(m % p.T);
-            kd[u] = sb * p.kv_bs + (p.kv_row0 + t_) * p.kv_rs;
-          }
-        }
-        V8 c1[4], c2[4], s1[4], s2[4];
-        if (rot) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            c1[u] = *reinterpret_cast<const V8*>(cosb + tp[u] * p.tab_rs);
-            c2[u] = *reinterpret_cast<const V8*>(cosb + tp[u] * p.tab_rs + 64);
-            s1[u] = *reinterpret_cast<const V8*>(sinb + tp[u] * p.tab_rs);
-            s2[u] = *reinterpret_cast<const V8*>(sinb + tp[u] * p.tab_rs + 64);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int ml = 8 * (4 * g + u) + r8;
-          const int m = mp + ml;
-          V8 x1 = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * c8) ^ swz(ml)) * 8));
-          V8 x2 = *reinterpret_cast<const V8*>(wl + ml * RB + (((16 + 2 * c8) ^ swz(ml)) * 8));
-          if (rot) {
-            V8 o1, o2;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const float a = (float)x1[i], b = (float)x2[i];
-              o1[i] = (T)(rnd<T>(a * (float)c1[u][i]) + rnd<T>(-b * (float)s1[u][i]));
-              o2[i] = (T)(rnd<T>(b * (float)c2[u][i]) + rnd<T>(a * (float)s2[u][i]));
-            }
-            x1 = o1;
-            x2 = o2;
-          }
-          if (to_out && m < p.M) {
-            *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + colw) = x1;
-            *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + colw + 64) = x2;
-          }
-          if (to_kv && m < p.rows) {
-            *reinterpret_cast<V8*>(kvb + kd[u]) = x1;
-            *reinterpret_cast<V8*>(kvb + kd[u] + 64) = x2;
-          }
-        }
-      }
+        for (int i = 0; i < 4; ++i) o[i] = (T)v[i];
+        *reinterpret_cast<V4*>(wl + ml * RB + (((4 * a + fg) ^ sw) * 8)) = o;
+      });
     } else {
-#pragma unroll 4
-      for (int j = 0; j < NRB; ++j) {
-        const int ml = RPI * j + rl;
-        const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
-        if (mp + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mp + ml) * p.ldo + col0) = v;
-      }
+      // gate tiles a = 0, 1, 4, 5 and their up tiles a + 2 (weight rows interleaved in blocks of 32): the wave's
+      // output columns are f = 32 (a >> 2) + 16 (a & 1) + 4 g + i of its 64
+      static_for<4>([&](auto ji) {
+        constexpr int a = (decltype(ji)::value & 1) + 4 * (decltype(ji)::value >> 1);
+        const f32x4 gv = acc4<4 * (8 * a + b)>(), uv = acc4<4 * (8 * (a + 2) + b)>();
+        V4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float g = rnd<T>(gv[i]), u = rnd<T>(uv[i]);
+          o[i] = (T)(rnd<T>(g / (1.0f + expf(-g))) * u);
+        }
+        const int unit = 8 * (a >> 2) + 4 * (a & 1) + fg;
+        *reinterpret_cast<V4*>(wl + ml * RB + ((unit ^ sw) * 8)) = o;
+      });
     }
   });
-  __syncthreads();                               // the epilogue's LDS reads are done before stage 1 is refilled
-  }                                              // next output tile
+  // each wave reads back only its own rows: its writes are ordered before its reads (no barrier needed)
+  T* ob = static_cast<T*>(p.out);
+  if constexpr (EPI == EPI_RESIDUAL) {
+#pragma unroll
+    for (int j = 0; j < NRB; ++j) {              // fully unrolled: rv stays in registers
+      const int ml = RPI * j + rl;
+      V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (T)((float)rv[j][i] + (float)v[i]);
+      if (mw + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mw + ml) * p.ldo + col0) = v;
+    }
+  } else if constexpr (EPI == EPI_ROPE) {
+    // read-back by rotation pairs: 8 lanes per row, lane c holds columns 8c.. and 64 + 8c.. of the wave's head;
+    // rope_kernel's arithmetic on the staged (rounded) projection, x1' = rnd(rnd(x1 c1) + rnd(-x2 s1)),
+    // x2' = rnd(rnd(x2 c2) + rnd(x1 s2)), table row pos[m] (or pos0 + m % T).  Rows go in groups of 4
+    // instructions whose table / index loads are all issued before the group's first use (one wait per group).
+    const bool rot = kind < 2;
+    const bool split = p.kout != nullptr;
+    const bool to_out = !split || kind == 0 || p.keep_k;        // keep_k: the k / v heads stay in out too
+    const bool to_kv = split && kind != 0;
+    const int c8 = lane & 7, r8 = lane >> 3;
+    T* const kvb = static_cast<T*>(kind == 2 ? p.vout : p.kout) +
+                   (int64_t)(hidx - p.hq - (kind == 2 ? p.hkv : 0)) * p.kv_hs + 8 * c8;
+    const int64_t colw = (int64_t)n0 + 128 * wn + 8 * c8;
+    const T* const cosb = static_cast<const T*>(p.cos_t) + 8 * c8;
+    const T* const sinb = static_cast<const T*>(p.sin_t) + 8 * c8;
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {
+      int64_t tp[4], kd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = mw + 8 * (4 * g + u) + r8;
+        const bool live = m < p.rows;
+        tp[u] = !live ? 0 : (p.pos ? p.pos[m] : p.pos0 + (int64_t)(m % p.T));
+        kd[u] = 0;
+        if (to_kv && live) {
+          const int64_t sb = p.dst_b ? p.dst_b[m] : (int64_t)(m / p.T);
+          const int64_t t = p.dst_b ? tp[u] : (int64_t)(m % p.T);
+          kd[u] = sb * p.kv_bs + (p.kv_row0 + t) * p.kv_rs;
+        }
+      }
+      V8 c1[4], c2[4], s1[4], s2[4];
+      if (rot) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          c1[u] = *reinterpret_cast<const V8*>(cosb + tp[u] * p.tab_rs);
+          c2[u] = *reinterpret_cast<const V8*>(cosb + tp[u] * p.tab_rs + 64);
+          s1[u] = *reinterpret_cast<const V8*>(sinb + tp[u] * p.tab_rs);
+          s2[u] = *reinterpret_cast<const V8*>(sinb + tp[u] * p.tab_rs + 64);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ml = 8 * (4 * g + u) + r8;
+        const int m = mw + ml;
+        V8 x1 = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * c8) ^ swz(ml)) * 8));
+        V8 x2 = *reinterpret_cast<const V8*>(wl + ml * RB + (((16 + 2 * c8) ^ swz(ml)) * 8));
+        if (rot) {
+          V8 o1, o2;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float a = (float)x1[i], b = (float)x2[i];
+            o1[i] = (T)(rnd<T>(a * (float)c1[u][i]) + rnd<T>(-b * (float)s1[u][i]));
+            o2[i] = (T)(rnd<T>(b * (float)c2[u][i]) + rnd<T>(a * (float)s2[u][i]));
+          }
+          x1 = o1;
+          x2 = o2;
+        }
+        if (to_out && m < p.M) {
+          *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + colw) = x1;
+          *reinterpret_cast<V8*>(ob + (int64_t)m * p.ldo + colw + 64) = x2;
+        }
+        if (to_kv && m < p.rows) {
+          *reinterpret_cast<V8*>(kvb + kd[u]) = x1;
+          *reinterpret_cast<V8*>(kvb + kd[u] + 64) = x2;
+        }
+      }
+    }
+  } else {
+#pragma unroll 4
+    for (int j = 0; j < NRB; ++j) {
+      const int ml = RPI * j + rl;
+      const V8 v = *reinterpret_cast<const V8*>(wl + ml * RB + (((2 * cl) ^ swz(ml)) * 8));
+      if (mw + ml < p.M) *reinterpret_cast<V8*>(ob + (int64_t)(mw + ml) * p.ldo + col0) = v;
+    }
+  }
 }
 
 // Split-K combine: out = epilogue(sum over the K ranges of the fp32 partials [splits][M][N], in range order — the
@@ -792,19 +717,6 @@ inline bool al16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 1
 
 namespace {
 
-// compute units of the current device (the persistent 4-wave kernel's grid: one workgroup per CU), cached per device
-int device_cus() {
-  static std::atomic<int> cache[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  int v = cache[dev].load(std::memory_order_relaxed);
-  if (v <= 0) {
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    cache[dev].store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
-
 // shared by cram_gemm and cram_gemm_residual: argument checks, then the 4-wave kernel (bf16, >= 2 K-tiles, 16-byte
 // output rows) or the 8-wave one
 int gemm_launch(GemmParams& p, int epi, int dtype, hipStream_t st) {
@@ -829,21 +741,14 @@ int gemm_launch(GemmParams& p, int epi, int dtype, hipStream_t st) {
   // K <= 4096: 1.02-1.03x the other order), groups of 8 weight tiles otherwise (down_proj: 1.07x; gate/up: equal)
   // (tools/gemm_ab_knob.py, r04); knob 2 forces the activation-tile groups, 1 the weight-tile groups (A/B)
   p.raster = kv == 2 ? 2 : (kv == 1 ? 0 : ((p.N <= 6144 && p.K <= 4096) ? 2 : 0));
-  // the 4-wave kernel is persistent: one workgroup per CU walks the tiles (gemm_w4_kernel); CRAM_W4_PERSISTENT=0
-  // launches one workgroup per tile instead (A/B: each workgroup then runs one tile, always with the full prologue)
-  static const bool persistent = [] {
-    const char* e = std::getenv("CRAM_W4_PERSISTENT");
-    return !(e && e[0] == '0');
-  }();
-  const dim3 gw((unsigned)(persistent ? std::min(p.nblocks, device_cus()) : p.nblocks));
   if (epi == EPI_ROPE) {                         // the 4-wave kernel only (the C-ABI checked bf16, kts >= 2)
-    hipLaunchKernelGGL((gemm_w4_kernel<__bf16, EPI_ROPE>), gw, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((gemm_w4_kernel<__bf16, EPI_ROPE>), g, dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
   }
   if (dtype == CRAM_DTYPE_BF16 && p.kts >= 2 && (p.ldo & 7) == 0 && kv != 0) {   // (16-byte output rows)
-    if (epi == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE>), gw, dim3(256), 0, st, p);
-    else if (epi == EPI_RESIDUAL) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, EPI_RESIDUAL>), gw, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL>), gw, dim3(256), 0, st, p);
+    if (epi == CRAM_GEMM_STORE) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_STORE>), g, dim3(256), 0, st, p);
+    else if (epi == EPI_RESIDUAL) hipLaunchKernelGGL((gemm_w4_kernel<__bf16, EPI_RESIDUAL>), g, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((gemm_w4_kernel<__bf16, CRAM_GEMM_SILU_MUL>), g, dim3(256), 0, st, p);
     return hipGetLastError() == hipSuccess ? CRAM_OK : CRAM_ERR_LAUNCH;
   }
   const dim3 blk(512);

@@ -177,24 +177,6 @@ def prologue():
     return lines
 
 
-def prologue_warm():
-    """Persistent form, every tile after a workgroup's first: tile 0 of this output tile was staged into stage 0 by the
-    previous tile's tail (before its epilogue; %[mx] / %[my] enter pointing at stage 1, %[so] at tile 1): stage tile 1,
-    wait for tile 0 (the epilogue's stores, issued in between, drain with it), read its k-step 0 fragments."""
-    lines = ["s_nop 4"]
-    for kind in ("y", "x"):
-        for _, g in dma_group(kind, step_apart=False):
-            for ln in g:
-                lines.append(ln)
-                if ln.startswith(("s_mov_b32 m0", "s_add_u32 m0")):
-                    lines.append("s_nop 0")
-    lines += ["s_waitcnt vmcnt(16)", "s_barrier"]
-    for f in range(8):
-        lines += [read("x", 0, f), read("y", 0, f)]
-    lines.append("s_waitcnt lgkmcnt(0)")
-    return lines
-
-
 def emit():
     out = ["// GENERATED by tools/gen_gemm_w4.py -- do not edit.  The main loop of gemm_w4_kernel (cram_gemm.hip).",
            "// Operands: see the generator's docstring.  Requires K-tiles per range >= 2.  TY: bf16 or f16 (a string literal)."]
@@ -203,13 +185,12 @@ def emit():
         for ln in lines:
             out.append(f'  "{ln}\\n\\t" \\')
 
-    for name, c, st, warm in ([(k, v, False, False) for k, v in VARIANTS.items()] + [("W", VENDOR, False, True)]
-                              + [("S", VENDOR, True, False)]):
+    for name, c, st in [(k, v, False) for k, v in VARIANTS.items()] + [("S", VENDOR, True)]:
         full, nodma, last = body(True, True, c, st), body(False, True, c, st), body(False, False, c, st)
-        out.append(f"// variant {name}" + (" (persistent: tile 0 already staged)" if warm else ""))
+        out.append(f"// variant {name}")
         out.append(f"#define CRAM_GEMM_W4_LOOP_{name}(TY) \\")
         put((["s_mov_b32 s80, 0", "s_mov_b32 s81, 0", "s_mov_b32 s82, 0", "s_mov_b32 s83, 0", "s_mov_b32 s84, 0"]
-             if st else []) + (prologue_warm() if warm else prologue()))
+             if st else []) + prologue())
         put(["s_cmp_eq_u32 %[n], 0", "s_cbranch_scc1 2f", "1:"])   # (the wrap's s_cmp sits before this one)
         put(full)
         put(["s_sub_u32 %[n], %[n], 1", "s_cmp_eq_u32 %[n], 0", "s_cbranch_scc0 1b", "2:"])
