@@ -77,7 +77,8 @@ int cram_abi_version(void);
  *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles and 16-byte output rows on the
  *                              4-wave 128 x 128-per-wave kernel (tile order by shape), others on the 8-wave kernel;
  *                              0 = the 8-wave kernel; 1 / 2 = the 4-wave kernel with weight-tile / activation-tile
- *                              groups (where it applies; otherwise as 0)
+ *                              groups (where it applies; otherwise as 0); cram_gemm_rope always runs the 4-wave
+ *                              kernel
  * cram_set_knob returns CRAM_ERR_INVALID_ARG for an unknown knob or value; cram_get_knob stores the value in
  * *value and returns CRAM_OK, or CRAM_ERR_INVALID_ARG for an unknown knob / null pointer (ABI 4: the value -1,
  * "automatic", is never an error code).
@@ -185,8 +186,10 @@ int cram_silu_mul(const void* gu, int64_t gu_rs, void* y, int64_t y_rs, int rows
                   cram_stream_t stream);
 
 /*
- * Projection GEMM of the engine (cram_gemm.hip; replaces F.linear / hipBLASLt for the MLP gate/up projection
- * and its activation: re_weighting.py:158,170 run them as nn.Linear inside every hooked forward).
+ * Projection GEMM of the engine (cram_gemm.hip; replaces F.linear / hipBLASLt for the sweep's and the packed
+ * prefill's projections and the elementwise op next to each -- the MLP activation here, the residual add and RoPE
+ * in cram_gemm_residual / cram_gemm_rope below: re_weighting.py:158,170 run them as nn.Linear inside every hooked
+ * forward).
  *   out[m, n] = sum_k y[m, k] * x[n, k]      y: activations [M][K] (row stride ldy), x: weights [N][K] (ldx),
  *   fp32 accumulation, bf16 / fp16 in and out; N % 256 == 0, K % 64 == 0, 16-byte aligned rows, any M >= 1.
  *   CRAM_GEMM_STORE      out [M][N] (ldo) = rnd(acc)
