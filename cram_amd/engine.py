@@ -734,7 +734,7 @@ class DecodeSession:
             h, x2 = eng.add_rmsnorm(self._proj(a.flatten(-2)[:, None], lw.wo, None, "o"), h, lw.ln2)
             m = self._mlp(x2, lw)
         _, hn = eng.add_rmsnorm(m[:, 0], h[:, 0], eng.norm)
-        nxt = self._pick(ops.gemm(hn, eng.lm_head, name="gemm") if self.lm_w4 else ops.linear(hn, eng.lm_head))
+        nxt = self._pick(ops.gemm(hn, eng.lm_head) if self.lm_w4 else ops.linear(hn, eng.lm_head))
         self.tokens.copy_(nxt)
         self.out.index_copy_(1, self.t.view(1), nxt[:, None])
         self.t.add_(1)
