@@ -480,7 +480,11 @@ def main():
                     pmc = json.load(open(PMC_FILE))
                     ratio = pmc["traffic_over_algorithmic"]
                     cur = _b.kernel_source_hash()
-                    if pmc.get("kernel_source_hash") == cur:
+                    same_kernel = f"{kname}(" in pmc.get("kernel", "") and result["dtype"] == "bf16"
+                    if pmc.get("kernel_source_hash") == cur and not same_kernel:
+                        roof["traffic_note"] = (f"PMC evidence {pmc['source']} was measured on {pmc.get('kernel')} "
+                                                f"(bf16): not this run's {kname} ({result['dtype']}), not applied")
+                    elif pmc.get("kernel_source_hash") == cur:
                         roof["traffic"] = round(ratio * roof["algorithmic_bytes_per_launch"])
                         roof["traffic_note"] = (f"HBM bytes/launch = PMC (FETCH_SIZEx2 + WRITE_SIZE, {pmc['source']}, "
                                                 f"kernel source {cur}) / algorithmic = {ratio:.4f} at the sweep shape "
