@@ -175,7 +175,8 @@ _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "
 # kernels that own accumulator registers by name inside their inline asm: prefill_x32_kernel (O = a[0:63],
 # Q = a[64:95]) and gemm_w4_kernel (all 256 accumulators a[0:255], its K loop one asm statement, the epilogue's
 # accumulator reads separate statements -- nothing of hipcc's may touch an AGPR in between; both instantiations)
-ASM_KERNELS = ("prefill_x32_kernel", "gemm_w4_kernelIDF16bLi0E", "gemm_w4_kernelIDF16bLi1E")
+ASM_KERNELS = ("prefill_x32_kernel", "gemm_w4_kernelIDF16bLi0E", "gemm_w4_kernelIDF16bLi1E", "gemm_w4_kernelIDF16_Li0E",
+               "gemm_w4_kernelIDF16_Li1E")
 ASM_SOURCES = ("cram_attn.hip", "cram_gemm.hip")
 
 

@@ -269,7 +269,7 @@ class CrAMEngine:
     FUSED_MLP_MIN_ROWS = 256
 
     def _fused_mlp_ok(self, x: torch.Tensor) -> bool:
-        if not FUSED_MLP or self.device.type != "cuda" or self.dtype != torch.bfloat16:
+        if not FUSED_MLP or self.device.type != "cuda" or self.dtype not in (torch.bfloat16, torch.float16):
             return False
         D, F = self.spec.hidden, self.spec.intermediate
         M = x.numel() // x.shape[-1]
@@ -597,8 +597,9 @@ class DecodeSession:
             # one partly filled row tile (config 5: 129 rows): q/k/v over 8 K ranges, 28 vs 41 us on hipBLASLt's pick
             # (Llama-3, tools/decode_gemm_probe.py --M 129, profiles/r04/dec129/); o_proj / gate/up stay on the library
             self.splits_gemm["qkv"] = 8 if D % (64 * 8) == 0 and qkv % 256 == 0 else 0
-        # lm_head on the 4-wave kernel (bf16, vocab % 256 == 0): 225 vs 290 us at 129 rows, 418 vs 457 at 512
-        self.lm_w4 = (eng.device.type == "cuda" and eng.dtype == torch.bfloat16 and eng.lm_head.shape[0] % 256 == 0
+        # lm_head on the 4-wave kernel (vocab % 256 == 0): 225 vs 290 us at 129 rows, 418 vs 457 at 512 (Llama-3)
+        self.lm_w4 = (eng.device.type == "cuda" and eng.dtype in (torch.bfloat16, torch.float16)
+                      and eng.lm_head.shape[0] % 256 == 0
                       and D % 64 == 0 and D >= 128 and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         shapes = {"qkv": qkv, "o": D, "gu": 2 * F, "down": D}
         need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in self.splits_gemm.items() if v]

@@ -74,7 +74,7 @@ int cram_abi_version(void);
  *                              one-wave-per-SIMD kernel, was removed in round 4: CRAM_ERR_INVALID_ARG)
  *   CRAM_KNOB_DECODE_U         -1 = by grid size; 1, 2, 4 = keys per lane group per iteration (VALU decode body)
  *   CRAM_KNOB_DECODE_MFMA      -1 / 1 = GQA groups of >= 4 heads at d = 128 decode on the matrix cores; 0 = VALU body
- *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: bf16 cram_gemm calls with >= 2 K-tiles and 16-byte output rows on the
+ *   CRAM_KNOB_GEMM_VARIANT     -1 = automatic: cram_gemm calls with >= 2 K-tiles and 16-byte output rows on the
  *                              4-wave 128 x 128-per-wave kernel (tile order by shape), others on the 8-wave kernel;
  *                              0 = the 8-wave kernel; 1 / 2 = the 4-wave kernel with weight-tile / activation-tile
  *                              groups (where it applies; otherwise as 0); cram_gemm_rope always runs the 4-wave
@@ -212,8 +212,8 @@ int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out,
  *   otherwise cram_rope_split: q rotated into out, k rotated into kout, v copied into vout; buffer row m < rows goes
  *   to sequence m / T, row kv_row0 + m % T, or with dst_b to dst_b[m], kv_row0 + pos[m] (strides kv_bs / kv_hs /
  *   kv_rs, elements); the k / v columns of out hold the rotated k and v if keep_k, else they are not written.
- * Rows in [rows, M) are GEMM padding: out rows written (q), nothing else.  bf16, d = 128, K % 64 == 0, K >= 128
- * (the 4-wave kernel), ldo % 8 == 0; pos / dst_b int64 device arrays of >= rows entries.  No bias (Llama).
+ * Rows in [rows, M) are GEMM padding: out rows written (q), nothing else.  bf16 / fp16, d = 128, K % 64 == 0,
+ * K >= 128 (the 4-wave kernel), ldo % 8 == 0; pos / dst_b int64 device arrays of >= rows entries.  No bias (Llama).
  */
 int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int K,
                    int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t, int64_t tab_rs,

@@ -85,7 +85,7 @@ def test_argument_validation_without_gpu():
     assert rope(kout=fake, vout=fake, dst_b=fake) == -1
     assert rope(kout=fake, vout=fake, rows=200, T=64) == -1
     assert rope(d=64) == -2
-    assert rope(dtype=1) == -2
+    assert rope(dtype=2) == -2
     assert rope(K=64) == -2
     assert rope(ldo=6148) == -3
     # split-K residual: residual checks, then split-K's (workspace)

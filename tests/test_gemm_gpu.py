@@ -271,25 +271,26 @@ def test_engine_fused_residual_layer_matches_deferred_add(gpu_device):
     assert d.max().item() <= 0.05 * lib.float().abs().max().item() and d.mean().item() <= 0.01 * scale, (d.max(), scale)
 
 
-def _rope_tables(P, d, dev, theta=500000.0):
+def _rope_tables(P, d, dev, theta=500000.0, dtype=torch.bfloat16):
     inv = 1.0 / theta ** (torch.arange(0, d, 2, dtype=torch.float32) / d)
     f = torch.arange(P, dtype=torch.float32)[:, None] * inv[None]
     emb = torch.cat((f, f), -1)
-    return emb.cos().to(torch.bfloat16).to(dev), emb.sin().to(torch.bfloat16).to(dev)
+    return emb.cos().to(dtype).to(dev), emb.sin().to(dtype).to(dev)
 
 
 HQ, HKV, HD = 32, 8, 128
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("K", [256, 4096])
-def test_gemm_rope_inplace_equals_gemm_then_rope(gpu_device, K):
+def test_gemm_rope_inplace_equals_gemm_then_rope(gpu_device, K, dtype):
     """cram_gemm_rope without kout (the sweep's suffix layers when no prefix is shared): bit-identical to the same
     kernel's plain GEMM followed by cram_rope_inplace over the q and k heads; v heads as computed; GEMM padding rows
     [rows, M) read table row 0 and are never compared."""
     B, T = 3, 1000
     rows, M = B * T, 3072
-    x, w = _operands(M, (HQ + 2 * HKV) * HD, K, torch.bfloat16, gpu_device, 41 + K)
-    cos, sin = _rope_tables(T, HD, gpu_device)
+    x, w = _operands(M, (HQ + 2 * HKV) * HD, K, dtype, gpu_device, 41 + K)
+    cos, sin = _rope_tables(T, HD, gpu_device, dtype=dtype)
     out = ops.gemm_rope(x, w, HQ, HKV, HD, cos, sin, T, rows=rows)
     ref = ops.gemm(x, w)
     ops.rope_inplace(ref[:rows], HQ + HKV, HD, cos, sin, T=T)
