@@ -90,9 +90,9 @@ FUSED_RESIDUAL = os.environ.get("CRAM_FUSED_RESIDUAL", "1") != "0"
 FUSED_QKV = os.environ.get("CRAM_FUSED_QKV", "1") != "0"
 # the sparse last wave of the residual GEMMs' tiles through split-K (CrAMEngine._gemm_residual); 0 = one launch (A/B)
 TAIL_SPLIT = os.environ.get("CRAM_TAIL_SPLIT", "1") != "0"
-# packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where the GEMMs already run at full rate; config 2
-# measured 75.75-75.94 q/s at 32k, 75.84 at 64k, 75.37 at 16k (r04, profiles/r04/ab_prefill_chunk/); CRAM_PREFILL_CHUNK_ROWS
-# overrides it (A/B)
+# packed-prefill chunk bound (tokens): the IE sweep's GEMM row count, where the GEMMs already run at full rate;
+# config 2 measured 75.75-75.94 q/s at 32k, 75.84 at 64k, 75.37 at 16k (r04, profiles/r04/ab_prefill_chunk/);
+# CRAM_PREFILL_CHUNK_ROWS overrides it (A/B)
 PREFILL_CHUNK_ROWS = int(os.environ.get("CRAM_PREFILL_CHUNK_ROWS", "32768"))
 
 
