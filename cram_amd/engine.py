@@ -513,6 +513,7 @@ DECODE_GEMM_MAX_ROWS = 512
 DECODE_GEMM_TARGET_WGS = 128
 DECODE_GEMM_MIN_K_OVER_N = 2
 DECODE_QKV_SPLIT_MAX_ROWS = 192
+DECODE_MLP_W4_MIN_ROWS = int(os.environ.get("CRAM_DECODE_MLP_W4_MIN_ROWS", "384"))
 
 
 def decode_splits(N: int, K: int, rows: int) -> int:
@@ -599,6 +600,14 @@ class DecodeSession:
             # one partly filled row tile (config 5: 129 rows): q/k/v over 8 K ranges, 28 vs 41 us on hipBLASLt's pick
             # (Llama-3, tools/decode_gemm_probe.py --M 129, profiles/r04/dec129/); o_proj / gate/up stay on the library
             self.splits_gemm["qkv"] = 8 if D % (64 * 8) == 0 and qkv % 256 == 0 else 0
+        # gate/up + SiLU-mul on the 4-wave kernel at >= 384 rows: 111.6 vs 116.6 us for hipBLASLt + cram_silu_mul at
+        # 512 rows (it loses at 129: 86 vs 64); the interleaved weight is built here, outside the step graph
+        self.mlp_w4 = (not self.splits_gemm["gu"] and self.B >= DECODE_MLP_W4_MIN_ROWS and eng.device.type == "cuda"
+                       and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))
+                       and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
+        if self.mlp_w4:
+            for lw in eng.layers:
+                eng._gate_up_interleaved(lw)
         # lm_head on the 4-wave kernel (vocab % 256 == 0): 225 vs 290 us at 129 rows, 418 vs 457 at 512 (Llama-3)
         self.lm_w4 = (eng.device.type == "cuda" and eng.dtype in (torch.bfloat16, torch.float16)
                       and eng.lm_head.shape[0] % 256 == 0
@@ -616,7 +625,9 @@ class DecodeSession:
 
     def _mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
         s = self.splits_gemm["gu"]
-        if s:
+        if self.mlp_w4:
+            act = ops.gemm(x, self.eng._gate_up_interleaved(lw), ops.GEMM_SILU_MUL)
+        elif s:
             act = ops.gemm_splitk(x, lw.wgu, s, ops.GEMM_SILU_MUL_CAT, workspace=self.gemm_ws)
         else:
             act = ops.silu_mul(ops.linear(x, lw.wgu), self.eng.spec.intermediate)

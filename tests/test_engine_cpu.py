@@ -321,7 +321,7 @@ def test_cpu_baseline_model_matches_engine(family):
     sp = ModelSpec(2, 256, 4, 2, 128, 512, 1000, 1e-5, family == "qwen2", family)
     eng = CrAMEngine.random(sp, torch.device("cpu"), seed=3, std=0.05)
     model = cpu_baseline.hf_model_from_engine(eng)
-    ids = torch.randint(0, 1000, (1, 77))
+    ids = torch.randint(0, 1000, (1, 77), generator=torch.Generator().manual_seed(77))
     w = torch.ones((1, 77), dtype=torch.float16)
     w[:, 10:30] = 0
     with torch.no_grad():
@@ -338,18 +338,26 @@ def test_cpu_baseline_model_matches_engine(family):
     d1 = cpu_baseline.time_decode(model, ids, w, {0: [1], 1: [0, 3]}, new_tokens=100, sampled_steps=2, layers=1)
     assert (d1["layers_run"], d1["layers"], d1["heads"]) == (1, 2, 1)
     assert len(model.model.layers) == 2 and model.config.num_hidden_layers == 2
-    # the hooked greedy ids of the sample equal the engine's batched decode with the same bias
+    # the hooked greedy ids of the sample equal the engine's batched decode with the same bias, up to the first
+    # near-tie (top-2 logit gap < 0.05: two bf16 evaluations of the same network may pick either)
     hs = hook_ref.register_hooks(model, {0: [1], 1: [0, 3]}, hook_ref.log_weight(w))
     try:
         with torch.no_grad():
-            ref_ids = model.generate(input_ids=ids, attention_mask=torch.ones_like(ids), do_sample=False,
-                                     max_new_tokens=4, min_new_tokens=4, pad_token_id=0)[0, 77:].tolist()
+            out = model.generate(input_ids=ids, attention_mask=torch.ones_like(ids), do_sample=False,
+                                 max_new_tokens=4, min_new_tokens=4, pad_token_id=0, output_scores=True,
+                                 return_dict_in_generate=True)
     finally:
         for h in hs:
             h.remove()
+    ref_ids = out.sequences[0, 77:].tolist()
+    gaps = [float(torch.topk(sc[0].float(), 2).values.diff().abs()) for sc in out.scores]
     with cpu_ops.patched_ops():
         got_ids = eng.generate([ids[0]], [w], {0: [1], 1: [0, 3]}, max_new_tokens=4, use_graph=False)[0]
-    assert got_ids == ref_ids
+    assert len(got_ids) == len(ref_ids) == 4
+    for t in range(4):
+        if got_ids[t] != ref_ids[t]:
+            assert min(gaps[:t + 1]) < 0.05, (t, got_ids, ref_ids, gaps)
+            break
 
 
 def test_sweep_prefix_skip_is_exact(tiny, nq):
