@@ -546,7 +546,7 @@ def main():
                 "data": f"synthetic: random-init {name} weights; rebuilt NQ-1000 prompts via offline BPE tokenizer",
                 "config": {"workload": f"{name} Find_Best_Heads IE sweep, {L} layers x {H} heads per question, "
                                        "scores [0,1,1,1,1], 1 NQ question per GPU per step (config 3; decode = config 2)",
-                           "model": model, "questions_per_step": world,
+                           "questions_per_step": world,
                            "question_order": "nearest the mean NQ prompt length first; steps x N questions dealt to "
                                              "ranks by cram_amd.dist.plan (LPT on token counts)",
                            "mean_prompt_tokens": round(ie["mean_T"], 1),
@@ -561,14 +561,14 @@ def main():
             if cpu:
                 result["speedup_vs_cpu"] = round(ie["value"] / cpu["value"], 1)
         else:
-            wl = {2: "Llama-3-8B NQ-1000 reweighted decode (top-894 heads, ideal scores)",
-                  4: "Qwen2-7B TriviaQA-1000 reweighted decode (all heads, ideal scores)",
-                  5: "Llama-3-8B NQ 20 retrieved docs (~8k tokens) reweighted decode (top-894 heads)"}[args.config]
+            wl = {2: f"{name} {dsname.upper()}-1000 reweighted decode ({heads_desc}, ideal scores)",
+                  4: f"{name} TriviaQA-1000 reweighted decode ({heads_desc}, ideal scores)",
+                  5: f"{name} NQ 20 retrieved docs (~8k tokens) reweighted decode ({heads_desc})"}[args.config]
             result.update({"metric": METRIC + f" [config {args.config}: decode]", "value": round(decode["value"], 3),
                            "unit": "questions/s", "ms_per_step": round(decode["seconds"] * 1e3 / decode["repeats"], 2),
                            "scaling": decode["scaling"],
                            "data": f"synthetic: random-init {model} weights; rebuilt {dsname} prompts",
-                           "config": {"workload": wl, "model": model, "questions": decode["questions"],
+                           "config": {"workload": wl, "questions": decode["questions"],
                                       "batch_per_gpu": decode["batch_per_gpu"],
                                       "new_tokens": decode["new_tokens"], "mean_prompt_tokens": decode["mean_prompt_tokens"],
                                       "parallelism": f"dp{world} replicas, each question decoded once "
@@ -658,7 +658,7 @@ def run_config1(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": "synthetic: random-init GPT-2-small weights; first 8 rebuilt NQ prompts (raw template)",
         "config": {"workload": "GPT-2-small, 8 NQ questions x 5 retrieved docs, batch-1 hooked-decode shape, all "
-                               "heads re-weighted, 32 new tokens", "model": "gpt2-small",
+                               "heads re-weighted, 32 new tokens",
                    "mean_prompt_tokens": round(T_mean, 1), "parallelism": "single GPU, batch 1"},
         "roofline": None, "cpu_baseline": cpu,
         "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None}), flush=True)
