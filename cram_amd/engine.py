@@ -600,9 +600,12 @@ class DecodeSession:
             # one partly filled row tile (config 5: 129 rows): q/k/v over 8 K ranges, 28 vs 41 us on hipBLASLt's pick
             # (Llama-3, tools/decode_gemm_probe.py --M 129, profiles/r04/dec129/); o_proj / gate/up stay on the library
             self.splits_gemm["qkv"] = 8 if D % (64 * 8) == 0 and qkv % 256 == 0 else 0
-        # gate/up + SiLU-mul on the 4-wave kernel at >= 384 rows: 111.6 vs 116.6 us for hipBLASLt + cram_silu_mul at
-        # 512 rows (it loses at 129: 86 vs 64); the interleaved weight is built here, outside the step graph
+        # gate/up + SiLU-mul on the 4-wave kernel at >= 384 rows for the Llama-3 MLP shape (N 28,672, K 4,096): 111.6 vs
+        # 116.6 us for hipBLASLt + cram_silu_mul at 512 rows; it loses at 129 rows (86 vs 64) and on Qwen2's shape
+        # (N 37,888, K 3,584: 167.8 vs 153.1; config 4 steps 13.9 -> 14.5 ms), profiles/r04/dec129/, decq/; the
+        # interleaved weight is built here, outside the step graph
         self.mlp_w4 = (not self.splits_gemm["gu"] and self.B >= DECODE_MLP_W4_MIN_ROWS and eng.device.type == "cuda"
+                       and 2 * sp.intermediate <= 28672 and sp.hidden >= 4096
                        and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))
                        and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         if self.mlp_w4:
