@@ -69,9 +69,9 @@ SIGNATURES = {
                           c_void_p]),
     "cram_gemm_residual": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int,
                                    c_int, c_int, c_int, c_void_p]),
-    "cram_gemm_rope": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int, c_int,
-                               c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p, c_int64,
-                               c_int64, c_int64, c_int, c_void_p, c_int, c_int, c_void_p]),
+    "cram_gemm_rope": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int, c_int, c_int,
+                               c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int64, c_void_p, c_int, c_void_p,
+                               c_void_p, c_int64, c_int64, c_int64, c_int, c_void_p, c_int, c_int, c_void_p]),
     "cram_gemm_splitk_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "cram_gemm_splitk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int,
                                  c_int, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),

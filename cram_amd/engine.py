@@ -85,7 +85,7 @@ FUSED_MLP = os.environ.get("CRAM_FUSED_MLP", "1") != "0"
 # o_proj / down_proj with the residual add in cram_gemm's epilogue (CrAMEngine.o_proj_norm / mlp_residual) at the same
 # row counts; CRAM_FUSED_RESIDUAL=0: the add inside the next RMSNorm instead (A/B)
 FUSED_RESIDUAL = os.environ.get("CRAM_FUSED_RESIDUAL", "1") != "0"
-# q/k/v projection with RoPE in cram_gemm's epilogue (bf16, head_dim 128, no q/k/v bias) at the same row counts;
+# q/k/v projection (+ bias) with RoPE in cram_gemm's epilogue (head_dim 128) at the same row counts;
 # CRAM_FUSED_QKV=0: hipBLASLt + cram_rope_inplace / cram_rope_split (A/B)
 FUSED_QKV = os.environ.get("CRAM_FUSED_QKV", "1") != "0"
 # the sparse last wave of the residual GEMMs' tiles through split-K (CrAMEngine._gemm_residual); 0 = one launch (A/B)
@@ -309,7 +309,7 @@ class CrAMEngine:
 
     def _fused_qkv_ok(self, x: torch.Tensor, lw: LayerW) -> bool:
         sp = self.spec
-        return (FUSED_QKV and lw.bqkv is None and self._fused_mlp_ok(x) and sp.head_dim == 128
+        return (FUSED_QKV and self._fused_mlp_ok(x) and sp.head_dim == 128
                 and (sp.num_heads + 2 * sp.num_kv_heads) % 2 == 0)
 
     def _fused_residual_ok(self, x: torch.Tensor) -> bool:
@@ -331,7 +331,8 @@ class CrAMEngine:
         """x [B, T, D] -> roped q [B, T, Hq, d], k / v [B, T, Hkv, d]: strided views of one fused buffer."""
         sp = self.spec
         if self._fused_qkv_ok(x, lw) and x.is_contiguous():
-            y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T=x.shape[-2], pos=pos)
+            y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T=x.shape[-2], pos=pos,
+                              bias=lw.bqkv)
         else:
             y = ops.linear(x, lw.wqkv, lw.bqkv)
             ops.rope_inplace(y, sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=y.shape[-2], pos=pos)
@@ -382,7 +383,8 @@ class CrAMEngine:
         fused = self._fused_qkv_ok(x, lw)            # RoPE in the q/k/v GEMM's epilogue (cram_gemm_rope)
         if prefix is None:
             if fused:
-                y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M)
+                y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M,
+                                  bias=lw.bqkv)
             else:
                 y = ops.linear(x, lw.wqkv, lw.bqkv)
                 ops.rope_inplace(y[:M], sp.num_heads + sp.num_kv_heads, sp.head_dim, cos, sin, T=T)
@@ -400,7 +402,7 @@ class CrAMEngine:
             if fused:
                 # the suffix rows' positions are p0 + t (the pos array's content): no position loads
                 y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M,
-                                  kout=k, vout=v, row0=p0, pos0=p0)
+                                  kout=k, vout=v, row0=p0, pos0=p0, bias=lw.bqkv)
             else:
                 y = ops.linear(x, lw.wqkv, lw.bqkv)
                 ops.rope_split(y[:M], sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)
@@ -699,7 +701,7 @@ class DecodeSession:
             kc, vc = self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2)
             if eng._fused_qkv_ok(x, lw):
                 y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
-                                  rows=total, kout=kc, vout=vc, row0=0, pos=pos, dst_b=bidx, keep_k=True)
+                                  rows=total, kout=kc, vout=vc, row0=0, pos=pos, dst_b=bidx, keep_k=True, bias=lw.bqkv)
             else:
                 y = ops.linear(x, lw.wqkv, lw.bqkv)
                 ops.rope_split(y[:total], sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1, kc, vc,

@@ -420,13 +420,14 @@ def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int
               sin: torch.Tensor, T: int, rows: Optional[int] = None, kout: Optional[torch.Tensor] = None,
               vout: Optional[torch.Tensor] = None, row0: int = 0, pos: Optional[torch.Tensor] = None,
               dst_b: Optional[torch.Tensor] = None, keep_k: bool = False, out: Optional[torch.Tensor] = None,
-              pos0: int = 0, name: str = "cram_gemm") -> torch.Tensor:
+              pos0: int = 0, bias: Optional[torch.Tensor] = None, name: str = "cram_gemm") -> torch.Tensor:
     """The q | k | v projection x @ w^T with RoPE in the GEMM epilogue (cram_gemm_rope, the 4-wave kernel; bf16,
     head_dim 128, no bias).  Without kout / vout: ``rope_inplace`` over the q and k heads of the result (T, pos as
     there; without pos the table row is pos0 + m % T).  With them: ``rope_split`` into kout / vout ([B, S, hkv, d]
     views, row0, pos, dst_b, keep_k as there),
     for the first ``rows`` rows of x (default all; rows beyond are GEMM padding).  Returns the [M, N] buffer: q
-    rotated; k rotated and v as computed unless kout is given without keep_k (then those columns are not written)."""
+    rotated; k rotated and v as computed unless kout is given without keep_k (then those columns are not written).
+    bias [N] (Qwen2's q/k/v): the projection is rnd(x @ w^T + bias) before RoPE, as F.linear rounds it."""
     _dt(x)
     if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
         raise ValueError("w must be a [N, K] row-major weight of x's dtype")
@@ -454,12 +455,15 @@ def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int
         if dst_b is not None and (pos is None or dst_b.dtype != torch.int64 or dst_b.numel() < rows
                                   or dst_b.device != x.device):
             raise ValueError("dst_b needs pos and must be a device int64 tensor with one entry per row")
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != N or not bias.is_contiguous()
+                             or bias.device != x.device):
+        raise ValueError("bias must be a contiguous [N] device tensor of x's dtype")
     if out is None:
         out = torch.empty(x.shape[:-1] + (N,), dtype=x.dtype, device=x.device)
     o2 = _rows2d(out, "out")
     ev = TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * N), x.device) if TIMER.enabled else None
     st = (0, 0, 0) if kout is None else (kout.stride(0), kout.stride(2), kout.stride(1))
-    code = _lib.load().cram_gemm_rope(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), o2.data_ptr(),
+    code = _lib.load().cram_gemm_rope(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), _ptr(bias), o2.data_ptr(),
                                       o2.stride(0), M, K, rows, int(T), int(hq), int(hkv), int(head_dim),
                                       cos.data_ptr(), sin.data_ptr(), cos.stride(0), _ptr(pos), int(pos0), _ptr(kout),
                                       _ptr(vout), st[0], st[1], st[2], int(row0), _ptr(dst_b), int(bool(keep_k)),

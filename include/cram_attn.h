@@ -213,12 +213,13 @@ int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out,
  *   to sequence m / T, row kv_row0 + m % T, or with dst_b to dst_b[m], kv_row0 + pos[m] (strides kv_bs / kv_hs /
  *   kv_rs, elements); the k / v columns of out hold the rotated k and v if keep_k, else they are not written.
  * Rows in [rows, M) are GEMM padding: out rows written (q), nothing else.  bf16 / fp16, d = 128, K % 64 == 0,
- * K >= 128 (the 4-wave kernel), ldo % 8 == 0; pos / dst_b int64 device arrays of >= rows entries.  No bias (Llama).
+ * K >= 128 (the 4-wave kernel), ldo % 8 == 0; pos / dst_b int64 device arrays of >= rows entries.  bias [N]
+ * (16-byte aligned; Qwen2's q / k / v) or NULL: the projection is rnd(acc + bias), F.linear's rounding, before RoPE.
  */
-int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int K,
-                   int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t, int64_t tab_rs,
-                   const int64_t* pos, int pos0, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs, int64_t kv_rs,
-                   int kv_row0, const int64_t* dst_b, int keep_k, int dtype, cram_stream_t stream);
+int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* bias, void* out, int64_t ldo,
+                   int M, int K, int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t,
+                   int64_t tab_rs, const int64_t* pos, int pos0, void* kout, void* vout, int64_t kv_bs, int64_t kv_hs,
+                   int64_t kv_rs, int kv_row0, const int64_t* dst_b, int keep_k, int dtype, cram_stream_t stream);
 
 /*
  * The same GEMM with the decoder layer's residual add in its epilogue (o_proj and down_proj: the residual

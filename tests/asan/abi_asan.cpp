@@ -112,11 +112,11 @@ static void validation_paths() {
   EXPECT(cram_gemm_residual(f, 64, f, 64, fc + 16, 256, f, 256, 1, 256, 64, 0, nullptr) == CRAM_ERR_INVALID_ARG);
   EXPECT(cram_gemm_residual(f, 64, f, 64, g, 260, f, 256, 1, 256, 64, 0, nullptr) == CRAM_ERR_ALIGNMENT);
   EXPECT(cram_gemm_residual(f, 64, f, 64, g, 256, f, 256, 1, 200, 64, 0, nullptr) == CRAM_ERR_UNSUPPORTED);
-  EXPECT(cram_gemm_rope(f, 128, f, 128, f, 6144, 256, 128, 257, 256, 32, 8, 128, f, f, 128, nullptr, 0, nullptr,
+  EXPECT(cram_gemm_rope(f, 128, f, 128, nullptr, f, 6144, 256, 128, 257, 256, 32, 8, 128, f, f, 128, nullptr, 0, nullptr,
                         nullptr, 0, 0, 0, 0, nullptr, 0, 0, nullptr) == CRAM_ERR_INVALID_ARG);
-  EXPECT(cram_gemm_rope(f, 128, f, 128, f, 6144, 256, 128, 256, 256, 32, 8, 64, f, f, 128, nullptr, 0, nullptr,
+  EXPECT(cram_gemm_rope(f, 128, f, 128, nullptr, f, 6144, 256, 128, 256, 256, 32, 8, 64, f, f, 128, nullptr, 0, nullptr,
                         nullptr, 0, 0, 0, 0, nullptr, 0, 0, nullptr) == CRAM_ERR_UNSUPPORTED);
-  EXPECT(cram_gemm_rope(f, 128, f, 128, f, 6144, 256, 128, 256, 256, 32, 8, 128, f, f, 128, nullptr, 0, f,
+  EXPECT(cram_gemm_rope(f, 128, f, 128, nullptr, f, 6144, 256, 128, 256, 256, 32, 8, 128, f, f, 128, nullptr, 0, f,
                         nullptr, 0, 0, 0, 0, nullptr, 0, 0, nullptr) == CRAM_ERR_INVALID_ARG);
   // error strings and knobs
   for (int c = 1; c >= -7; --c) EXPECT(cram_strerror(c) != nullptr && std::strlen(cram_strerror(c)) > 0);

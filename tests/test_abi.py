@@ -77,8 +77,8 @@ def test_argument_validation_without_gpu():
     # q/k/v + RoPE GEMM: tables, rows <= M, kout / vout together, dst_b needs pos, bf16 and head dim 128 only
     def rope(M=256, K=128, rows=256, T=256, d=128, cos=fake, kout=None, vout=None, dst_b=None, pos=None, dtype=0,
              ldo=6144):
-        return L.cram_gemm_rope(fake, K, fake, K, fake, ldo, M, K, rows, T, 32, 8, d, cos, fake, 128, pos, 0, kout,
-                                vout, 0, 0, 0, 0, dst_b, 0, dtype, None)
+        return L.cram_gemm_rope(fake, K, fake, K, None, fake, ldo, M, K, rows, T, 32, 8, d, cos, fake, 128, pos, 0,
+                                kout, vout, 0, 0, 0, 0, dst_b, 0, dtype, None)
     assert rope(cos=None) == -1
     assert rope(rows=257) == -1
     assert rope(kout=fake) == -1
@@ -88,6 +88,8 @@ def test_argument_validation_without_gpu():
     assert rope(dtype=2) == -2
     assert rope(K=64) == -2
     assert rope(ldo=6148) == -3
+    assert L.cram_gemm_rope(fake, 128, fake, 128, fake + 8, fake, 6144, 256, 128, 256, 256, 32, 8, 128, fake, fake, 128,
+                            None, 0, None, None, 0, 0, 0, 0, None, 0, 0, None) == -3      # misaligned bias
     # split-K residual: residual checks, then split-K's (workspace)
     ws4 = L.cram_gemm_splitk_workspace_size(16, 512, 4)
     assert L.cram_gemm_splitk_residual(fake, 512, fake, 512, None, 512, fake, 512, 16, 512, 512, 4, fake, ws4, 0,

@@ -298,6 +298,31 @@ def test_gemm_rope_inplace_equals_gemm_then_rope(gpu_device, K, dtype):
     assert torch.equal(out[:rows], ref[:rows])
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemm_rope_bias(gpu_device, dtype):
+    """cram_gemm_rope with Qwen2's q/k/v bias: the projection is rnd(acc + bias) (F.linear's rounding) before RoPE.
+    With identity tables (cos 1, sin 0) the result is that projection itself: within the final-rounding bar of the
+    float32 product plus the bias; with real tables it equals RoPE applied to it (cram_rope_inplace)."""
+    B, T, K = 2, 700, 512
+    rows, M = B * T, 1536
+    N = (HQ + 2 * HKV) * HD
+    x, w = _operands(M, N, K, dtype, gpu_device, 53)
+    b = (torch.rand(N, generator=torch.Generator().manual_seed(4)) - 0.5).to(dtype).to(gpu_device)
+    one = torch.ones(T, HD, dtype=dtype, device=gpu_device)
+    zero = torch.zeros(T, HD, dtype=dtype, device=gpu_device)
+    proj = ops.gemm_rope(x, w, HQ, HKV, HD, one, zero, T, rows=rows, bias=b)
+    ref = x.float() @ w.float().t() + b.float()
+    acc_tol = 2.0 ** -22 * (x.float().abs() @ w.float().abs().t())
+    cos, sin = _rope_tables(T, HD, gpu_device, dtype=dtype)
+    out = ops.gemm_rope(x, w, HQ, HKV, HD, cos, sin, T, rows=rows, bias=b)
+    exp = proj.clone()
+    ops.rope_inplace(exp[:rows], HQ + HKV, HD, cos, sin, T=T)
+    torch.cuda.synchronize()
+    d = (proj[:rows].float() - ref[:rows]).abs()
+    assert (d <= _ulp(ref[:rows], dtype) + acc_tol[:rows]).all(), float(d.max())
+    assert torch.equal(out[:rows], exp[:rows])
+
+
 def test_gemm_rope_split_behind_prefix(gpu_device):
     """The sweep's layer_rows with a shared prefix: q rotated in place, k rotated into and v copied into the
     [B, p0 + T] key / value buffers behind the prefix at table rows pos = p0 + t; == GEMM + cram_rope_split, the
@@ -346,12 +371,13 @@ def test_gemm_rope_split_into_cache_keep_k(gpu_device):
     assert torch.equal(kc, kcr) and torch.equal(vc, vcr)
 
 
-def test_engine_fused_qkv_layer_matches_library_path(gpu_device):
+@pytest.mark.parametrize("qkv_bias", [False, True])
+def test_engine_fused_qkv_layer_matches_library_path(gpu_device, qkv_bias):
     """CrAMEngine.layer_rows at sweep row counts with RoPE in the q/k/v GEMM's epilogue == the library path
     (hipBLASLt + cram_rope_split) within the bf16 noise of two GEMM accumulation orders, with and without a shared
-    prefix."""
+    prefix; Llama (no bias) and Qwen2 (q/k/v bias in the epilogue)."""
     from cram_amd import engine as E
-    sp = E.ModelSpec(2, 1024, 8, 2, 128, 1536, 1000, 1e-5, False)
+    sp = E.ModelSpec(2, 1024, 8, 2, 128, 1536, 1000, 1e-5, qkv_bias)
     eng = E.CrAMEngine.random(sp, gpu_device, seed=13, std=0.03)
     B, T, p0 = 9, 500, 20
     gen = torch.Generator(device=gpu_device).manual_seed(5)
