@@ -118,7 +118,8 @@ def decode_leg_roofline(spec, phases, dtype):
                       "ms_per_step": round(st_ms / max(1, n_steps), 3), "bytes_per_step": st_bytes / max(1, n_steps),
                       "weight_bytes_per_step": w_bytes},
             "graph_capture_ms": round(cap_ms / len(phases), 2),
-            "note": "HIP events on the launch stream inside engine.generate, summed over the timed repeats"}
+            "note": "HIP events on the launch stream inside engine.generate: each rate is the timed batches' summed "
+                    "work over their summed time; the ms fields are means per decode batch (ms_per_step per step)"}
 
 
 def log(*a):
@@ -164,7 +165,10 @@ def main():
                     help="decode scores: ideal [0.1,1,1,1,1] or the NQ GPT truthful scores (RAG_test.py:89-105)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefix-skip", action="store_true", help="recompute rows before the first biased key (A/B)")
-    ap.add_argument("--cpu-units", type=int, default=8, help="IE units of the CPU baseline sample (>= 1)")
+    ap.add_argument("--cpu-units", type=int, default=64,
+                    help="IE units of the CPU baseline sample (>= 1; BASELINE.md: 1 question x 2 layers x 32 heads)")
+    ap.add_argument("--cpu-decode-questions", type=int, default=2,
+                    help="questions of the CPU decode baseline's sample (BASELINE.md: 2 NQ questions)")
     ap.add_argument("--cpu-decode-steps", type=int, default=8,
                     help="decode steps of the CPU decode baseline's sample (0 = skip it); extrapolated to --decode-tokens")
     ap.add_argument("--cpu-decode-layers", type=int, default=-1,
@@ -400,9 +404,9 @@ def main():
             decode["attention_roofline"] = decode_attention_roofline(eng, [dev_prompts[i] for i in b0],
                                                                      [ws[i] for i in b0], heads, args.decode_tokens,
                                                                      dev)
-        # the CPU baseline's question: the one nearest the mean prompt length
-        qc = min(range(nq_dec), key=lambda i: (abs(lens[i] - T_mean), i))
-        dec_cpu_input = (qc, prompts[qc], ws[qc], heads)
+        # the CPU baseline's questions: the ones nearest the mean prompt length
+        qcs = sorted(range(nq_dec), key=lambda i: (abs(lens[i] - T_mean), i))[:max(1, args.cpu_decode_questions)]
+        dec_cpu_input = ([(qc, prompts[qc], ws[qc]) for qc in qcs], heads)
         log(f"[rank {rank}] decode: {decode['value']:.2f} questions/s ({nq_dec} questions, T mean {T_mean:.0f}); "
             f"decode attention {decode.get('attention_roofline', {}).get('achieved', 0):.0f} GB/s")
         del dev_prompts
@@ -423,37 +427,46 @@ def main():
             units_s = cpu_baseline.sample_units(L, H, max(1, args.cpu_units))
             r = cpu_baseline.time_ie_units(cpu_model, ids.cpu(), w, ans.cpu(), units_s)
             sp_ = r["spread"]
+            lay_s = sorted(set(l for l, _ in units_s))
             cpu = {"value": r["units_per_s"], "unit": "heads/s", "cores": r["cores"], "kind": "port",
-                   "sample": f"{r['units']} IE units {units_s} over {len(set(l for l, _ in units_s))} layers (hooked "
-                             f"full forward + full-vocab logits + .item(), re_weighting.py:162-171) of NQ question {qi} "
-                             f"at T'={ids.numel()}, after 1 un-hooked forward; {r['seconds']:.1f}s; {result['dtype']} "
-                             f"torch CPU; extrapolates linearly per unit",
+                   "sample": f"{r['units']} IE units = 1 question x {len(lay_s)} layers {lay_s} x "
+                             f"{len(set(h for _, h in units_s))} heads (hooked full forward + full-vocab logits + "
+                             f".item(), re_weighting.py:162-171) of NQ question {qi} at T'={ids.numel()}, after 1 "
+                             f"un-hooked forward; {r['seconds']:.1f}s; {result['dtype']} torch CPU; extrapolates "
+                             f"linearly per unit",
                    "unit_seconds": {"min": round(sp_["min_s"], 3), "median": round(sp_["median_s"], 3),
                                     "max": round(sp_["max_s"], 3)}}
             log(f"[rank 0] cpu baseline {cpu['value']:.4f} heads/s on {cpu['cores']} cores")
         if want_dec:
-            qc, ids, w, hd = dec_cpu_input
-            # long prompts (config 5, ~8k tokens): the hooked forward builds a dense [H, T, T] mask per hooked layer,
-            # minutes per question on the host, so the sample runs the first 2 layers and scales per layer
-            k_layers = args.cpu_decode_layers if args.cpu_decode_layers >= 0 else (2 if ids.numel() > 4096 else 0)
-            r = cpu_baseline.time_decode(cpu_model, ids.cpu(), w, hd if hd else
-                                         {l: list(range(H)) for l in range(L)},
-                                         new_tokens=args.decode_tokens, sampled_steps=args.cpu_decode_steps,
-                                         layers=k_layers, log=log)
-            cpu_dec = {"value": r["questions_per_s"], "unit": "questions/s", "cores": r["cores"], "kind": "port",
+            qlist, hd = dec_cpu_input
+            runs = []
+            for qc, ids, w in qlist:
+                # long prompts (config 5, ~8k tokens): the hooked forward builds a dense [H, T, T] mask per hooked
+                # layer, minutes per question on the host, so the sample runs the first 2 layers and scales per layer
+                k_layers = args.cpu_decode_layers if args.cpu_decode_layers >= 0 else (2 if ids.numel() > 4096 else 0)
+                r = cpu_baseline.time_decode(cpu_model, ids.cpu(), w, hd if hd else
+                                             {l: list(range(H)) for l in range(L)},
+                                             new_tokens=args.decode_tokens, sampled_steps=args.cpu_decode_steps,
+                                             layers=k_layers, log=log)
+                runs.append((qc, r))
+            tot_s = sum(r["question_s"] for _, r in runs)
+            r = runs[0][1]
+            cpu_dec = {"value": len(runs) / tot_s, "unit": "questions/s", "cores": r["cores"], "kind": "port",
                        "method": "sampled + extrapolated",
-                       "sample": (f"1 question ({dsname} #{qc}, {r['prompt_tokens']} prompt tokens, {r['heads']} "
+                       "sample": (f"{len(runs)} question(s) ({dsname} #{', #'.join(str(q) for q, _ in runs)}: "
+                                  f"{', '.join(str(x['prompt_tokens']) for _, x in runs)} prompt tokens, {r['heads']} "
                                   f"hooked heads"
                                   + (f" in the first {r['layers_run']} of {r['layers']} layers, times scaled by "
                                      f"{r['layers']}/{r['layers_run']}" if r["layers_run"] < r["layers"] else "")
                                   + "): hooks on the selected heads + greedy generate "
-                                  f"(re_weighting.py:115-138) of 1 + {r['sampled_steps']} tokens, {r['seconds']:.1f}s; "
-                                  f"prefill {r['prefill_s']:.2f}s + {args.decode_tokens - 1} x median step "
-                                  f"{r['step_s']['median']:.3f}s = {r['question_s']:.1f}s per question at "
-                                  f"{args.decode_tokens} new tokens; {result['dtype']} torch CPU, batch 1 as the "
-                                  f"reference"),
-                       "prefill_s": round(r["prefill_s"], 3),
-                       "step_seconds": {k: round(v, 4) for k, v in r["step_s"].items()}}
+                                  f"(re_weighting.py:115-138) of 1 + {r['sampled_steps']} tokens each, "
+                                  f"{sum(x['seconds'] for _, x in runs):.1f}s; per question prefill + "
+                                  f"{args.decode_tokens - 1} x median step = "
+                                  f"{', '.join('%.1f' % x['question_s'] for _, x in runs)}s at {args.decode_tokens} new "
+                                  f"tokens; value = questions / summed seconds; {result['dtype']} torch CPU, batch 1 "
+                                  f"as the reference"),
+                       "prefill_s": [round(x["prefill_s"], 3) for _, x in runs],
+                       "step_seconds": [{k: round(v, 4) for k, v in x["step_s"].items()} for _, x in runs]}
             decode["cpu_baseline"] = cpu_dec
             decode["speedup_vs_cpu"] = round(decode["value"] / cpu_dec["value"], 1)
             log(f"[rank 0] cpu decode baseline {cpu_dec['value']:.5f} questions/s on {cpu_dec['cores']} cores")

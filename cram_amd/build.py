@@ -19,7 +19,7 @@ CSRC = PKG_DIR / "csrc"
 LIB_PATH = PKG_DIR / "libcram_attn.so"
 SOURCES = [CSRC / "cram_attn.hip", CSRC / "cram_fused.hip", CSRC / "cram_gemm.hip", CSRC / "cram_spans.cpp"]
 HEADERS = [REPO_DIR / "include" / "cram_attn.h", CSRC / "prefill_asm.inc", CSRC / "prefill_x32.inc",
-           CSRC / "gemm_w4_loop.inc"]
+           CSRC / "gemm_w4_loop.inc", CSRC / "cram_silu.inc"]
 ARCH = "gfx950"
 
 
@@ -92,7 +92,7 @@ def _build(objdir: Path, verbose: bool) -> Path:
     if failed:
         raise subprocess.CalledProcessError(1, failed[0])
     asm = "\n".join(asm_path(src).read_text() for src in ASM_SOURCES)
-    for kname in ASM_KERNELS:
+    for kname in asm_kernels(asm):
         bad = audit_asm_kernel(asm, kname)
         if bad:
             raise RuntimeError(f"{kname} register audit failed (the library is not installed): " + "; ".join(bad[:5]))
@@ -144,7 +144,8 @@ def gemm_source_hash() -> str:
     evidence (profiles/gemm_pmc.json) records it, and bench.py applies that evidence only while it matches."""
     import hashlib
     h = hashlib.sha256()
-    for f in (CSRC / "cram_gemm.hip", CSRC / "gemm_w4_loop.inc", REPO_DIR / "include" / "cram_attn.h"):
+    for f in (CSRC / "cram_gemm.hip", CSRC / "gemm_w4_loop.inc", CSRC / "cram_silu.inc",
+              REPO_DIR / "include" / "cram_attn.h"):
         h.update(f.read_bytes())
     return h.hexdigest()[:16]
 
@@ -155,7 +156,8 @@ def x64_asm_path() -> Path:
 
 
 def kernel_body(asm: str, name: str) -> str:
-    m = re.search(r"^(_Z\w*" + name + r"\w*):", asm, re.M)
+    m = re.search(r"^(" + name + r"):", asm, re.M) if name.startswith("_Z") else \
+        re.search(r"^(_Z\w*" + name + r"\w*):", asm, re.M)
     if not m:
         raise RuntimeError(f"kernel {name} not found in the assembly")
     return asm[m.end(): asm.find(".Lfunc_end", m.end())]
@@ -173,15 +175,26 @@ _NO_DST = ("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop", "
 
 
 # kernels that own accumulator registers by name inside their inline asm: prefill_x32_kernel (O = a[0:63],
-# Q = a[64:95]) and gemm_w4_kernel (all 256 accumulators a[0:255], its K loop one asm statement, the epilogue's
-# accumulator reads separate statements -- nothing of hipcc's may touch an AGPR in between; both instantiations)
-ASM_KERNELS = ("prefill_x32_kernel", "gemm_w4_kernelIDF16bLi0E", "gemm_w4_kernelIDF16bLi1E", "gemm_w4_kernelIDF16_Li0E",
-               "gemm_w4_kernelIDF16_Li1E")
+# Q = a[64:95]) and every instantiation of gemm_w4_kernel (all 256 accumulators a[0:255], its K loop one asm
+# statement, the epilogue's accumulator reads separate statements -- nothing of hipcc's may touch an AGPR in between).
+# The list is not written by hand: `asm_kernels` takes every symbol whose name contains one of these stems from the
+# assembly, so a new epilogue or element type is audited as soon as it is instantiated.
+ASM_KERNEL_STEMS = ("prefill_x32_kernel", "gemm_w4_kernel")
 ASM_SOURCES = ("cram_attn.hip", "cram_gemm.hip")
 
 
+def asm_kernels(asm: str) -> list:
+    """Every kernel symbol of the assembly whose name contains one of ASM_KERNEL_STEMS (mangled names, sorted)."""
+    stems = "|".join(ASM_KERNEL_STEMS)
+    names = sorted(set(re.findall(r"^(_Z\w*(?:" + stems + r")\w*):", asm, re.M)))
+    for stem in ASM_KERNEL_STEMS:
+        if not any(stem in n for n in names):
+            raise RuntimeError(f"no {stem} symbol in the assembly: the register audit no longer matches the sources")
+    return names
+
+
 def audit_asm_kernel(asm: str, kname: str = "prefill_x32_kernel") -> list:
-    """The kernels of ASM_KERNELS own accumulator registers by name inside their inline asm (prefill_x32_kernel:
+    """The kernels of `asm_kernels` own accumulator registers by name inside their inline asm (prefill_x32_kernel:
     O = a[0:63], Q = a[64:95]; gemm_w4_kernel: a[0:255]); hipcc knows nothing of that.
     Returns the violations in kernel `kname` (empty = clean):
       * any v_accvgpr_* / AGPR operand the COMPILER emitted (outside the kernel's ;;#ASMSTART..;;#ASMEND blocks);

@@ -371,9 +371,10 @@ class CrAMEngine:
         is the layer output, the add ran in down_proj's epilogue).
         out_rows=n returns [B*n, D] pairs (last n rows of every sequence).
 
-        prefix=(k0, v0, pos): the B sequences are SUFFIXES that start at position p0 = k0.shape[1] of a common
-        prefix whose roped K/V at this layer are k0/v0 [1, p0, Hkv, d] (shared by all B sequences); pos is the
-        int64 [B*T] position of every row.  Attention then runs over p0 + T keys per sequence."""
+        prefix=(k0, v0): the B sequences are SUFFIXES that start at position p0 = k0.shape[1] of a common
+        prefix whose roped K/V at this layer are k0/v0 [1, p0, Hkv, d] (shared by all B sequences); row t of every
+        suffix sits at position p0 + t (the only form: the fused path computes that position, the library path
+        builds the same array).  Attention then runs over p0 + T keys per sequence."""
         sp, lw = self.spec, self.layers[l]
         M = B * T
         if delta is None:
@@ -392,7 +393,7 @@ class CrAMEngine:
             k = y3[..., sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
             v = y3[..., sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))
         else:                                        # [prefix | suffix] keys per sequence
-            k0, v0, pos = prefix
+            k0, v0 = prefix
             p0 = k0.shape[1]
             k = torch.empty((B, p0 + T, sp.num_kv_heads, sp.head_dim), dtype=self.dtype, device=self.device)
             v = torch.empty_like(k)
@@ -400,11 +401,12 @@ class CrAMEngine:
             v[:, :p0] = v0
             # q roped in place; the suffix's roped k and its v land behind the prefix (no copy pass)
             if fused:
-                # the suffix rows' positions are p0 + t (the pos array's content): no position loads
+                # the suffix rows' positions are p0 + t: no position loads
                 y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M,
                                   kout=k, vout=v, row0=p0, pos0=p0, bias=lw.bqkv)
             else:
                 y = ops.linear(x, lw.wqkv, lw.bqkv)
+                pos = (torch.arange(T, device=self.device, dtype=torch.int64) + p0).repeat(B)
                 ops.rope_split(y[:M], sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)
             y3 = y[:M].view(B, T, -1)
         q = y3[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
@@ -607,7 +609,7 @@ class DecodeSession:
         # (N 37,888, K 3,584: 167.8 vs 153.1; config 4 steps 13.9 -> 14.5 ms), profiles/r04/dec129/, decq/; the
         # interleaved weight is built here, outside the step graph
         self.mlp_w4 = (not self.splits_gemm["gu"] and self.B >= DECODE_MLP_W4_MIN_ROWS and eng.device.type == "cuda"
-                       and 2 * sp.intermediate <= 28672 and sp.hidden >= 4096
+                       and (2 * sp.intermediate, sp.hidden) == (28672, 4096)     # the measured shape only
                        and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))
                        and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         if self.mlp_w4:

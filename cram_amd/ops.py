@@ -421,8 +421,8 @@ def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int
               vout: Optional[torch.Tensor] = None, row0: int = 0, pos: Optional[torch.Tensor] = None,
               dst_b: Optional[torch.Tensor] = None, keep_k: bool = False, out: Optional[torch.Tensor] = None,
               pos0: int = 0, bias: Optional[torch.Tensor] = None, name: str = "cram_gemm") -> torch.Tensor:
-    """The q | k | v projection x @ w^T with RoPE in the GEMM epilogue (cram_gemm_rope, the 4-wave kernel; bf16,
-    head_dim 128, no bias).  Without kout / vout: ``rope_inplace`` over the q and k heads of the result (T, pos as
+    """The q | k | v projection x @ w^T with RoPE in the GEMM epilogue (cram_gemm_rope, the 4-wave kernel; bf16 or
+    fp16, head_dim 128, optional q/k/v bias).  Without kout / vout: ``rope_inplace`` over the q and k heads of the result (T, pos as
     there; without pos the table row is pos0 + m % T).  With them: ``rope_split`` into kout / vout ([B, S, hkv, d]
     views, row0, pos, dst_b, keep_k as there),
     for the first ``rows`` rows of x (default all; rows beyond are GEMM padding).  Returns the [M, N] buffer: q

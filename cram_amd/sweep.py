@@ -118,11 +118,8 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     h, m = eng.mlp_residual(x2, lw, h)                                  # layer output h (+ m when deferred)
     if not last:
         cos, sin = eng.rope_tables(T_full)
-        pos = None
-        if p0 > 0:
-            pos = (torch.arange(T, device=eng.device, dtype=torch.int64) + p0).repeat(Hv)
         for l2 in range(l + 1, L):
-            pre = None if p0 == 0 else (qc.k[l2][:, :p0], qc.v[l2][:, :p0], pos)
+            pre = None if p0 == 0 else (qc.k[l2][:, :p0], qc.v[l2][:, :p0])         # suffix row t at p0 + t
             h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m,
                                   prefix=pre)
     rows = Hv * n_ans

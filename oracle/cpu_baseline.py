@@ -110,12 +110,22 @@ def time_ie_units(model, ids: torch.Tensor, w16: torch.Tensor, answer_ids: torch
 
 
 def sample_units(num_layers: int, num_heads: int, n: int):
-    """n (layer, head) units spread over the layers (first, last, middle, quarters, ...) and heads."""
+    """n (layer, head) units: whole layers of all heads (BASELINE.md's plan: 1 question x 2 layers x 32 heads = 64
+    units), the layers taken in the spread order first, last, middle, quarters, ...; a count that is not a multiple
+    of the head count ends with the first heads of one more layer.  (In the reference every unit is one full hooked
+    forward whatever its layer, re_weighting.py:162-171, so the layers only spread the sample.)"""
     fr = [0.0, 1.0, 0.5, 0.25, 0.75, 0.125, 0.625, 0.375, 0.875]
+    order = []
+    for f in fr + [i / num_layers for i in range(num_layers)]:
+        l = int(round(f * (num_layers - 1)))
+        if l not in order:
+            order.append(l)
     out = []
-    for i in range(n):
-        l = round(fr[i % len(fr)] * (num_layers - 1)) if i < len(fr) else (i * 7) % num_layers
-        out.append((int(l), int((i * 11 + 3) % num_heads)))
+    for l in order:
+        for h in range(num_heads):
+            if len(out) == n:
+                return out
+            out.append((l, h))
     return out
 
 

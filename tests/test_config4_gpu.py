@@ -4,10 +4,10 @@ depth is irrelevant to the kernels, the widths are not) — on one rebuilt Trivi
 [0.1, 1, 1, 1, 1] re-ordered as RAG_test.py:64-107 orders them, all heads re-weighted: layers_to_be_modified = {}).
 
 Pins the automatic GQA-7 choices together at the config's shape: the 7-wave prefill workgroups (hp7, <= 2048 tokens),
-the matrix-core decode for 7-head groups and the decode step's split-K down projection (the engine's rule routes only
-long-K projections through cram_gemm_splitk: at this shape K = 3584 < 2N for q/k/v, so the q/k/v bias runs in the
-library GEMM), and — with CRAM_DECODE_GEMM=all, which routes every decode projection through the split-K kernel — the
-q/k/v bias added in the split-K combine, against
+the matrix-core decode for 7-head groups and the decode step's split-K projections (the engine's rule routes long-K
+down_proj through cram_gemm_splitk, and at <= DECODE_QKV_SPLIT_MAX_ROWS rows -- this test's 2 -- q/k/v over 8 K ranges
+with the q/k/v bias added in the split-K combine), and -- with CRAM_DECODE_GEMM=all, which routes every decode
+projection through the split-K kernel -- the same for o_proj and gate/up, against
   * the transformers drop-in on the same kernels (greedy ids up to the first near-tie, re_weighting.py:127-132);
   * the reference hook itself (oracle/hook_ref.py, dense mask, bf16 transformers) and the float32 truth (same hook
     on the float32 copy of the weights): re-weighted answer log-probs of the drop-in and of the engine within

@@ -385,9 +385,8 @@ def test_engine_fused_qkv_layer_matches_library_path(gpu_device, qkv_bias):
     cos, sin = eng.rope_tables(p0 + T)
     k0 = torch.randn(1, p0, sp.num_kv_heads, sp.head_dim, device=gpu_device, generator=gen).to(torch.bfloat16)
     v0 = torch.randn_like(k0)
-    pos = (torch.arange(T, device=gpu_device, dtype=torch.int64) + p0).repeat(B)
     assert eng._fused_qkv_ok(h, eng.layers[1])
-    for pre in (None, (k0, v0, pos)):
+    for pre in (None, (k0, v0)):
         fused = eng.layer_rows(h, B, T, 1, cos, sin, prefix=pre)
         prev = E.FUSED_QKV
         E.FUSED_QKV = False
