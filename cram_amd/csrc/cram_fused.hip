@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(const T* __restrict__ gu,
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float x = (float)g[j];
-    const float s = rnd<T>(cram_silu(x));
+    const float s = rnd<T>(cram_silu<T>(x));
     o[j] = (T)(s * (float)u[j]);
   }
   *reinterpret_cast<V8*>(y + row * y_rs + c) = o;

@@ -452,7 +452,8 @@ class CrAMEngine:
     def generate(self, prompts: Sequence[torch.Tensor], weights16: Sequence[torch.Tensor], layers_to_heads: dict,
                  max_new_tokens: int = 100, eos_ids: Sequence[int] = (), bad_token_ids: Sequence[int] = (),
                  use_graph: bool = True, stop_on_eos: bool = True,
-                 repetition_penalty: float = 1.0, phases: Optional[dict] = None) -> List[List[int]]:
+                 repetition_penalty: float = 1.0, phases: Optional[dict] = None,
+                 bad_words_ids: Sequence[Sequence[int]] = ()) -> List[List[int]]:
         """Greedy decode of several prompts at once (per-row lengths, per-row credibility bias).
 
         Returns the generated ids of every prompt, truncated after its first EOS
@@ -460,6 +461,9 @@ class CrAMEngine:
         one-at-a-time generation as in re_weighting.py:127-132).  repetition_penalty != 1 applies transformers'
         RepetitionPenaltyLogitsProcessor (the checkpoint's generation_config, e.g. Qwen chat models ship 1.05)
         over each row's prompt and generated ids.
+        bad_words_ids: transformers' NoBadWordsLogitsProcessor (generate(bad_words_ids=...), re_weighting.py:128-129):
+        a one-id sequence is banned at every step, a longer one bans its last id whenever the row's ids so far (prompt
+        + generated) end with its other ids; bad_token_ids = one-id sequences.
         phases: a dict that receives HIP events on the launch stream around the packed prefill, the step-graph
         capture and the decode steps ("t0", "prefill", "capture", "steps") plus the step count and the session's
         row lengths, for timing the leg's phases without a host sync inside it.
@@ -468,7 +472,8 @@ class CrAMEngine:
         if ev is not None:
             phases["t0"] = ev()
             phases["t0"].record()
-        sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids,
+        sess = DecodeSession(self, prompts, weights16, layers_to_heads, max_new_tokens,
+                             [[int(t)] for t in bad_token_ids] + [list(map(int, s)) for s in bad_words_ids],
                              repetition_penalty)
         sess.prefill()
         if ev is not None:
@@ -556,7 +561,7 @@ def decode_attn_splits(B: int, num_kv_heads: int, S_max: int) -> int:
 class DecodeSession:
     """Static-shape state of one batched greedy decode (KV cache, bias, token buffers)."""
 
-    def __init__(self, eng: CrAMEngine, prompts, weights16, layers_to_heads, max_new_tokens, bad_token_ids=(),
+    def __init__(self, eng: CrAMEngine, prompts, weights16, layers_to_heads, max_new_tokens, bad_words=(),
                  repetition_penalty: float = 1.0):
         sp = eng.spec
         self.eng = eng
@@ -577,7 +582,30 @@ class DecodeSession:
         self.seq_lens = torch.tensor(self.lens, dtype=torch.int32, device=dev)     # keys visible after the write
         self.out = torch.zeros((self.B, max_new_tokens), dtype=torch.long, device=dev)
         self.t = torch.zeros((), dtype=torch.long, device=dev)                    # next output column
-        self.bad = torch.tensor(list(bad_token_ids), dtype=torch.long, device=dev) if bad_token_ids else None
+        # bad words (transformers' NoBadWordsLogitsProcessor): one-id sequences are banned at every step; a sequence of
+        # n > 1 ids bans its last id while the row's last n - 1 ids (prompt + generated, kept in `hist`) equal its first
+        # n - 1 -- all on the device, inside the captured step
+        single = sorted({s[0] for s in bad_words if len(s) == 1})
+        multi = sorted({tuple(s) for s in bad_words if len(s) > 1})
+        if any(len(s) == 0 for s in bad_words):
+            raise ValueError("empty bad-words sequence")
+        self.bad = torch.tensor(single, dtype=torch.long, device=dev) if single else None
+        self.bw_pre = self.bw_valid = self.bw_last = self.hist = None
+        if multi:
+            Lm = max(len(s) for s in multi) - 1
+            pre = torch.full((len(multi), Lm), -1, dtype=torch.long)
+            valid = torch.zeros((len(multi), Lm), dtype=torch.bool)
+            for i, s in enumerate(multi):                 # right-aligned: column Lm - 1 is the id just before
+                pre[i, Lm - (len(s) - 1):] = torch.tensor(s[:-1])
+                valid[i, Lm - (len(s) - 1):] = True
+            hist = torch.full((self.B, Lm), -1, dtype=torch.long)
+            for b, p in enumerate(self.prompts):
+                tail = p[-Lm:].cpu()
+                hist[b, Lm - tail.numel():] = tail
+            # a sequence longer than the row's ids so far never matches (HF skips it): the -1 fill matches no id
+            self.bw_pre, self.bw_valid = pre.to(dev), valid.to(dev)
+            self.bw_last = [s[-1] for s in multi]
+            self.hist = hist.to(dev)
         # repetition penalty (transformers RepetitionPenaltyLogitsProcessor): the set of ids each row has seen so
         # far (prompt + generated) as a [B, V] mask, updated inside the (graph-captured) step
         self.penalty = float(repetition_penalty)
@@ -649,7 +677,19 @@ class DecodeSession:
             logits = torch.where(seen, torch.where(x < 0, x * self.penalty, x / self.penalty), x)
         if self.bad is not None:
             logits = logits.index_fill(-1, self.bad, float("-inf"))
+        if self.hist is not None:
+            h = self.hist if rows is None else self.hist[rows]
+            match = ((h[:, None, :] == self.bw_pre[None]) | ~self.bw_valid[None]).all(-1)        # [rows, sequences]
+            logits = logits.clone() if self.bad is None else logits
+            for i, t in enumerate(self.bw_last):
+                logits[:, t] = torch.where(match[:, i], float("-inf"), logits[:, t])
         nxt = torch.argmax(logits, dim=-1)
+        if self.hist is not None:                 # the rows' ids so far, shifted by the new one
+            new = torch.cat([h[:, 1:], nxt[:, None]], 1)
+            if rows is None:
+                self.hist.copy_(new)
+            else:
+                self.hist[rows] = new
         if self.seen is not None:             # scatter of a scalar: no host tensor, capturable in the step graph
             (self.seen if rows is None else self.seen[rows]).scatter_(1, nxt[:, None], True)
         return nxt
@@ -766,7 +806,7 @@ class DecodeSession:
         s.wait_stream(torch.cuda.current_stream(self.eng.device))
         # warm the allocator / kernels on a side stream, then restore the state it advanced
         snap = (self.tokens.clone(), self.pos.clone(), self.seq_lens.clone(), self.t.clone(), self.out.clone(),
-                None if self.seen is None else self.seen.clone())
+                None if self.seen is None else self.seen.clone(), None if self.hist is None else self.hist.clone())
         with gemm_tune.pinned(decode=True), torch.cuda.stream(s):
             self._step_body()
         torch.cuda.current_stream(self.eng.device).wait_stream(s)
@@ -774,6 +814,8 @@ class DecodeSession:
         self.t.copy_(snap[3]); self.out.copy_(snap[4])
         if self.seen is not None:
             self.seen.copy_(snap[5])
+        if self.hist is not None:
+            self.hist.copy_(snap[6])
         self.graph = torch.cuda.CUDAGraph()
         with gemm_tune.pinned(decode=True), torch.cuda.graph(self.graph):
             self._step_body()

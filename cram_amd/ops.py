@@ -474,6 +474,40 @@ def gemm_rope(x: torch.Tensor, w: torch.Tensor, hq: int, hkv: int, head_dim: int
     return out
 
 
+def gemm_small(x: torch.Tensor, w: torch.Tensor, splits: int = 1, epilogue: int = GEMM_STORE,
+               bias: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+               out: Optional[torch.Tensor] = None, name: str = "cram_gemm_small") -> torch.Tensor:
+    """x [..., K] @ w[N, K]^T (+ bias) on the decode-step GEMM (cram_gemm_small: 128 x 128 tiles, a four-deep LDS
+    ring; few rows); GEMM_SILU_MUL takes the interleaved gate/up weight (interleave_gate_up) and returns [..., N/2].
+    splits > 1 cuts K into ranges combined in order through `workspace` (a uint8 device tensor of
+    >= gemm_splitk_workspace_bytes(M, N, splits); allocated here when None, pass one for hipGraph capture)."""
+    _dt(x)
+    if w.dtype != x.dtype or w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("w must be a [N, K] row-major weight of x's dtype")
+    x2 = _rows2d(x, "x")
+    M, K = x2.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError(f"K mismatch: x {K}, w {w.shape[1]}")
+    if bias is not None and (bias.dtype != x.dtype or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous [N] tensor of x's dtype")
+    nout = N if epilogue == GEMM_STORE else N // 2
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (nout,), dtype=x.dtype, device=x.device)
+    o2 = _rows2d(out, "out")
+    if splits > 1 and workspace is None:
+        workspace = torch.empty(gemm_splitk_workspace_bytes(M, N, splits), dtype=torch.uint8, device=x.device)
+    ev = (TIMER.record(name, 2.0 * M * N * K, 2.0 * (M * K + N * K + M * nout), x.device) if TIMER.enabled else None)
+    code = _lib.load().cram_gemm_small(x2.data_ptr(), x2.stride(0), w.data_ptr(), w.stride(0), _ptr(bias),
+                                       o2.data_ptr(), o2.stride(0), M, N, K, int(splits), int(epilogue),
+                                       _ptr(workspace), 0 if workspace is None else workspace.numel(), _dt(x),
+                                       _stream(x.device))
+    _lib.check(code, "cram_gemm_small")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(x.device))
+    return out
+
+
 def gemm_splitk_workspace_bytes(M: int, N: int, splits: int) -> int:
     return int(_lib.load().cram_gemm_splitk_workspace_size(int(M), int(N), int(splits)))
 

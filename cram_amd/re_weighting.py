@@ -169,11 +169,11 @@ class Re_Weighting_Strategy:
         penalty = self._greedy_processors()
         eos = kw.get("eos_token_id", self.model.generation_config.eos_token_id)
         eos = [eos] if isinstance(eos, int) else list(eos or [])
-        bad = [b[0] for b in self.bad_words_ids if len(b) == 1]
-        if len(bad) != len(self.bad_words_ids):
-            raise NotImplementedError("multi-token bad_words_ids are not supported by the batched engine")
+        # generate(bad_words_ids=...) as transformers applies it (NoBadWordsLogitsProcessor): a one-id sequence equal
+        # to an EOS id is dropped, every other sequence (any length) is banned on the device inside the step
+        bad = [list(b) for b in self.bad_words_ids if not (len(b) == 1 and b[0] in eos)]
         gens = self.engine.generate(prompts, ws, self.layers_to_be_modified, max_new_tokens=max_new_tokens,
-                                    eos_ids=eos, bad_token_ids=bad, use_graph=use_graph, repetition_penalty=penalty)
+                                    eos_ids=eos, bad_words_ids=bad, use_graph=use_graph, repetition_penalty=penalty)
         res = []
         for ids, g in zip(prompts, gens):
             full = torch.cat([ids.cpu(), torch.tensor(g, dtype=ids.dtype)])

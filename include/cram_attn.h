@@ -48,9 +48,10 @@ extern "C" {
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
 
-#define CRAM_ABI_VERSION 5        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
+#define CRAM_ABI_VERSION 6        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
                                      4: cram_get_knob(which, *value), decode projection GEMM;
-                                     5: cram_gemm_residual, cram_gemm_rope, cram_gemm_splitk_residual */
+                                     5: cram_gemm_residual, cram_gemm_rope, cram_gemm_splitk_residual;
+                                     6: cram_gemm_small */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -246,6 +247,21 @@ size_t cram_gemm_splitk_workspace_size(int M, int N, int splits);
 int cram_gemm_splitk(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out, int64_t ldo, int M, int N,
                      int K, int splits, int epilogue, const void* bias, void* workspace, size_t ws_bytes, int dtype,
                      cram_stream_t stream);
+
+/*
+ * The decode step's projections (ABI 6): the same GEMM on 128 x 128 output tiles for few activation rows (M = the
+ * decode batch, ~128-512: re_weighting.py:127-132 runs q/k/v, o_proj, the MLP and lm_head inside generate, one token
+ * per row per step), where 256 x 256 tiles leave most CUs idle; a four-deep LDS ring keeps three K-tiles of the
+ * weights (streamed from HBM once per step) in flight.  K is cut into `splits` equal ranges (K % (64 * splits) == 0);
+ * splits > 1 writes fp32 partial sums to the workspace ([splits][M][N], cram_gemm_splitk_workspace_size bytes,
+ * 16-B aligned) and combines them in range order (deterministic).
+ *   CRAM_GEMM_STORE      out [M][N] (ldo) = rnd(acc + bias[n])   (bias [N], 16-B aligned, or NULL)
+ *   CRAM_GEMM_SILU_MUL   x = the interleaved gate/up weight of cram_gemm; out [M][N/2] = the MLP activation
+ * N % 128 == 0, 16-byte aligned rows, any M >= 1; ldo % 8 == 0 when splits > 1.
+ */
+int cram_gemm_small(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* bias, void* out, int64_t ldo,
+                    int M, int N, int K, int splits, int epilogue, void* workspace, size_t ws_bytes, int dtype,
+                    cram_stream_t stream);
 
 /*
  * Split-K with cram_gemm_residual's epilogue: out = rnd(res + rnd(sum)) (res may be out itself).  The engine runs the

@@ -17,6 +17,7 @@ import pytest
 import torch
 
 from oracle import hook_ref
+from tests import parity
 from tests import tiny_models as tm
 from tests.test_engine_cpu import ie_tolerance_check
 from tests.test_kernels_gpu import _check
@@ -275,7 +276,8 @@ def test_llama2_logprobs_match_reference_hook(path, nq, gpu_device):
         t = truth[(r["idx"], r["scores"], r["heads"])]
         ref_err = np.abs(np.array(r["logprobs"]) - t).max()
         err = np.abs(lp.cpu().numpy() - t)
-        assert err.max() <= 2.5 * ref_err + 0.01, (r["idx"], r["scores"], r["heads"], err.max(), ref_err)
+        parity.check("logprob_max", err.max(), ref_err, kind="llama2", idx=r["idx"], scores=r["scores"],
+                     heads=r["heads"])
 
 
 def test_llama2_engine_batched_decode(path, nq, gpu_device):

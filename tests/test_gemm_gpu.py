@@ -441,3 +441,59 @@ def test_engine_residual_gemm_tail_split(gpu_device, K):
     d = (out[rows].float() - (ref + h[rows].float())).abs()
     bar = _ulp(ref, torch.bfloat16) + _ulp(ref + h[rows].float(), torch.bfloat16) + acc_tol
     assert (d <= bar).all(), float(d.max())
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# cram_gemm_small: the decode step's projections (128 x 128 tiles, four-deep ring, optional K split)
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("M,N,K,splits", [
+    (1, 128, 64, 1), (5, 256, 192, 1), (129, 384, 4096, 1), (500, 6144, 4096, 1), (512, 4096, 4096, 2),
+    (128, 1024, 14336, 4), (200, 768, 3584, 7), (77, 512, 128, 2), (256, 640, 320, 5),
+])
+def test_gemm_small_matches_fp32(gpu_device, dtype, M, N, K, splits):
+    """Every tile / ring / K-split / tail path: single-tile K ranges (K = 64), ranges shorter than the ring
+    (2-3 K-tiles), the steady state, ragged M (rows past M read as zeros, never stored)."""
+    x, w = _operands(M, N, K, dtype, gpu_device, 3 * M + N + K + splits)
+    out = torch.full((M + 3, N), 7.0, dtype=dtype, device=gpu_device)
+    ops.gemm_small(x, w, splits, out=out[:M])
+    ref = x.float() @ w.float().t()
+    acc_tol = 2.0 ** -22 * (x.float().abs() @ w.float().abs().t())
+    torch.cuda.synchronize()
+    d = (out[:M].float() - ref).abs()
+    assert (d <= _ulp(ref, dtype) + acc_tol).all(), f"max err {d.max().item():.3e}"
+    assert (out[:M] == ref.to(dtype)).float().mean().item() >= 0.99
+    assert (out[M:] == 7).all()
+
+
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_small_bias_and_silu_mul(gpu_device, splits):
+    """F.linear with a bias (Qwen2's q/k/v: rnd(acc + b), the split-K combine's rule too) and the SiLU-mul epilogue
+    on the interleaved gate/up weight == the same GEMM stored, then cram_silu_mul (bit for bit, either split)."""
+    M, N, K, F = 300, 1024, 2048, 1024
+    x, w = _operands(M, N, K, torch.bfloat16, gpu_device, 11)
+    b = (torch.randn(N, device=gpu_device) * 0.5).to(torch.bfloat16)
+    out = ops.gemm_small(x, w, splits, bias=b)
+    ref = (x.float() @ w.float().t() + b.float())
+    torch.cuda.synchronize()
+    assert ((out.float() - ref).abs() <= _ulp(ref, torch.bfloat16) + 1e-5).all()
+    xg, wgu = _operands(M, 2 * F, K, torch.bfloat16, gpu_device, 12)
+    wil = ops.interleave_gate_up(wgu, F)
+    act = ops.gemm_small(xg, wil, splits, ops.GEMM_SILU_MUL)
+    plain = ops.gemm_small(xg, wgu, splits)
+    torch.cuda.synchronize()
+    assert torch.equal(act, ops.silu_mul(plain, F))
+
+
+def test_gemm_small_rejects_bad_arguments(gpu_device):
+    from cram_amd import _lib
+    x, w = _operands(64, 256, 256, torch.bfloat16, gpu_device, 1)
+    with pytest.raises(RuntimeError, match="CRAM error -2"):
+        ops.gemm_small(x, w[:200])                    # N % 128
+    with pytest.raises(RuntimeError, match="CRAM error -2"):
+        ops.gemm_small(x, w, 3)                       # K % (64 * splits)
+    L = _lib.load()
+    o = torch.empty(64, 256, dtype=torch.bfloat16, device=gpu_device)
+    code = L.cram_gemm_small(x.data_ptr(), 256, w.data_ptr(), 256, None, o.data_ptr(), 256, 64, 256, 256, 2,
+                             ops.GEMM_STORE, None, 0, 0, None)
+    assert code == -5                                 # CRAM_ERR_WORKSPACE: splits > 1 without a workspace

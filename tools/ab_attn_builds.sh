@@ -14,7 +14,8 @@ if git -C $R cat-file -e $REV:cram_amd/csrc/cram_gemm.hip 2>/dev/null; then
   git -C $R show $REV:cram_amd/csrc/cram_gemm.hip > $T/cram_amd/csrc/cram_gemm.hip
   SRCS="$SRCS $T/cram_amd/csrc/cram_gemm.hip"
 fi
-mkdir -p $R/tools/ablib
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I $T/include $SRCS -o $R/tools/ablib/libcram_base.so
+OUTDIR=${OUTDIR:-$R/tools/ablib}
+mkdir -p $OUTDIR
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I $T/include $SRCS -o $OUTDIR/libcram_base.so
 rm -rf $T
-echo $R/tools/ablib/libcram_base.so
+echo $OUTDIR/libcram_base.so

@@ -101,6 +101,23 @@ def main():
             finally:
                 _lib.set_knob(_lib.KNOB_GEMM_VARIANT, prev)
             res.append(("w4", t, err))
+        if N % 128 == 0 and K % 64 == 0:
+            # cram_gemm_small (128 x 128 tiles, four-deep ring): one pass and K splits; gate/up on the interleaved weight
+            # with the fused SiLU-mul
+            wil = [ops.interleave_gate_up(w, F) for w in ws_] if name == "gate_up" else None
+            for s in (1, 2, 3, 4, 7, 8):
+                if K % (64 * s) or ops.gemm_splitk_workspace_bytes(M, N, s) > ws.numel():
+                    continue
+                if name == "gate_up":
+                    fn = lambda w, s=s: ops.gemm_small(x, w, s, ops.GEMM_SILU_MUL, workspace=ws)
+                    err = float((fn(wil[0]).float() - ops.silu_mul(ref.to(torch.bfloat16), F).float()).abs().max())
+                    t = timeit(fn, wil)
+                else:
+                    fn = lambda w, s=s: ops.gemm_small(x, w, s, workspace=ws)
+                    err = float((fn(ws_[0]).float() - ref).abs().max())
+                    t = timeit(fn, ws_)
+                res.append((f"sm{s}", t, err))
+            del wil
         for r in res:
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "method": r[0], "us": round(r[1], 2),
                               "weight_TBps": round(wbytes / r[1] / 1e6, 3),

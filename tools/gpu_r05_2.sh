@@ -1,0 +1,20 @@
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/r05/g2
+mkdir -p $O
+timeout -k 10 300 python -u tools/ab_gemm_builds.py tools/abbase/libcram_base.so cram_amd/libcram_attn.so 29184 5 > $O/ab_gemm.txt 2>&1
+grep -v Warning $O/ab_gemm.txt | tail -12
+timeout -k 10 300 python -u -m pytest tests/test_gemm_gpu.py -m gpu -x -q -k small --timeout 120 --timeout-method thread > $O/small_tests.txt 2>&1
+tail -2 $O/small_tests.txt
+for m in 512 128; do
+  timeout -k 10 300 python -u tools/decode_gemm_probe.py --M $m > $O/probe_llama3_M$m.txt 2>&1
+  grep -v amdgpu.ids $O/probe_llama3_M$m.txt | python3 -c "
+import sys,json
+for l in sys.stdin:
+    try: r=json.loads(l)
+    except Exception: continue
+    print(r['shape'], r['M'], r['method'], r['us'])"
+done
+timeout -k 10 300 python -u tools/decode_gemm_probe.py --model qwen2 --M 512 > $O/probe_qwen2_M512.txt 2>&1
+CRAM_PARITY_LOG=$PWD/$O/parity.jsonl timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/gputest.txt 2>&1 || echo "pytest rc=$?"
+tail -8 $O/gputest.txt
