@@ -345,6 +345,9 @@ def main():
         s_max = max(lens) + args.decode_tokens
         per_row = 2 * spec.num_layers * spec.num_kv_heads * s_max * spec.head_dim * 2
         cap = max(1, int(0.55 * torch.cuda.get_device_properties(dev).total_memory // per_row))
+        # whole 64-row groups when the budget binds: the decode step's projections run on 128-row tiles
+        # (cram_gemm_small), so one row past a multiple of 128 would cost a whole extra tile (config 5: 129 -> 128)
+        cap = cap // 64 * 64 if cap >= 128 else cap
         B = min(args.decode_batch, cap)
         if B < args.decode_batch:
             log(f"[rank {rank}] decode batch {args.decode_batch} -> {B} (KV cache {per_row / 2**20:.0f} MiB per row)")

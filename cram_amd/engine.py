@@ -547,6 +547,28 @@ def decode_splits(N: int, K: int, rows: int) -> int:
     return best
 
 
+# Decode-step projections on cram_gemm_small (128 x 128 tiles, K split so the grid fills the CUs) at one 128-row
+# activation tile: config 5's batch and every GPU's share of NQ-1000 at 8 GPUs.  Measured at 128 rows, Llama-3 widths
+# (tools/decode_gemm_probe.py --M 128, profiles/r05/dec128/): q/k/v 22.8 vs 26.3 us (hipBLASLt), o_proj 18.8 vs 24.6,
+# down_proj 34.6 vs 47.2 (the 8-wave split-K); gate/up (61-63 vs 60) and lm_head (the 4-wave kernel, 206 vs 246) stay.
+# At 512 rows it loses (q/k/v 43-52 vs 42): a 128 x 128 tile moves twice the bytes per MFMA of a 256 x 256 one, and a
+# CU pulls only ~30 GB/s from beyond its L2.
+DECODE_SMALL_MAX_ROWS = 128
+
+
+def small_splits(N: int, K: int, rows: int) -> int:
+    """K ranges of cram_gemm_small for one decode projection, or 0 (not routed there): the most ranges that keep
+    N / 128 column tiles x ranges within the 256 CUs with >= 4 K-tiles per range."""
+    if (os.environ.get("CRAM_DECODE_GEMM", "1") == "0" or rows > DECODE_SMALL_MAX_ROWS or N % 128 or K % 64):
+        return 0
+    ntn, kt = N // 128, K // 64
+    best = 0
+    for s in range(1, kt + 1):
+        if kt % s == 0 and ntn * s <= 256 and kt // s >= 4:
+            best = s
+    return best
+
+
 def decode_attn_splits(B: int, num_kv_heads: int, S_max: int) -> int:
     """Split-S count of the decode attention: enough (batch row, kv head) work items x splits to cover ~512
     workgroups, at most 16 splits and at least 256 keys per split; long rows (>= 4096 keys) take at least 2 while
@@ -647,12 +669,21 @@ class DecodeSession:
         self.lm_w4 = (eng.device.type == "cuda" and eng.dtype in (torch.bfloat16, torch.float16)
                       and eng.lm_head.shape[0] % 256 == 0
                       and D % 64 == 0 and D >= 128 and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
+        # one activation tile: q/k/v, o_proj and down_proj on cram_gemm_small with the K split that fills the CUs (the
+        # split-K / library picks above are then unused for them)
+        kin = {"qkv": D, "o": sp.q_size, "down": F}
         shapes = {"qkv": qkv, "o": D, "gu": 2 * F, "down": D}
-        need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in self.splits_gemm.items() if v]
-                   or [0])
+        self.small = {k: small_splits(shapes[k], kin[k], self.B) for k in kin} if eng.device.type == "cuda" else {}
+        self.small = {k: v for k, v in self.small.items() if v}
+        for k in self.small:
+            self.splits_gemm[k] = 0
+        need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in
+                    list(self.splits_gemm.items()) + list(self.small.items()) if v] or [0])
         self.gemm_ws = torch.empty(need, dtype=torch.uint8, device=dev) if need else None
 
     def _proj(self, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], key: str) -> torch.Tensor:
+        if key in self.small:
+            return ops.gemm_small(x, w, self.small[key], ops.GEMM_STORE, bias=b, workspace=self.gemm_ws)
         s = self.splits_gemm[key]
         if s:
             return ops.gemm_splitk(x, w, s, ops.GEMM_STORE, bias=b, workspace=self.gemm_ws)

@@ -1,18 +1,27 @@
 """The noise-floor parity bars of the float-valued outputs, written once.
 
 Every bar compares our error against the float32 truth (the reference hook on the float32 copy of the same weights)
-with the reference algorithm's own 16-bit error on the same sample:  ours <= F * reference + A.
+with the reference algorithm's own 16-bit error on the same sample:
   ie_mean / ie_max   the IE grid of cal_logits (re_weighting.py:152-175): mean / max over the grid of |IE - truth|
   logprob_max        the re-weighted answer-token log-probabilities (the hooked forward of re_weighting.py:118-127):
                      max over the answer tokens of |log p - truth|
-Achieved ratios (ours / reference) are appended, one JSON line per check, to the file CRAM_PARITY_LOG names (the
-suites' evidence run: profiles/r05/parity_ratios.json summarises it); F and A below come from that evidence.
+Two bars per family:
+  * per sample, a guard against gross errors: ours <= GUARD_F * reference + GUARD_A[family].  A single sample's ratio
+    is ill-conditioned -- the reference's own error on one tiny-model question can be near zero (measured ratios up
+    to 3.5 on samples whose reference error is 0.005) -- so this bar alone has no teeth;
+  * per test, over all its samples (the teeth): sum(ours) <= AGG_F[family] * sum(reference).  AGG_F is the worst
+    aggregate ratio measured on the GPU suite + 25 % (profiles/r05/parity_ratios.json), at most 1.5: an error that
+    doubles fails it.  The CPU suite's stand-in kernels (tests/cpu_ops.py: fp32 CPU math, not the product's
+    arithmetic) have their own measured aggregates (AGG_F_CPU).
+Every check appends one JSON line to the file CRAM_PARITY_LOG names (the evidence runs).
 """
 import json
 import os
 
-# (F, A) per family
-BARS = {"ie_mean": (2.5, 0.01), "ie_max": (2.5, 0.05), "logprob_max": (2.5, 0.01)}
+GUARD_F = 4.0
+GUARD_A = {"ie_mean": 0.01, "ie_max": 0.05, "logprob_max": 0.01}
+AGG_F = {"ie_mean": 1.5, "ie_max": 1.5, "logprob_max": 1.5}
+AGG_F_CPU = {"ie_mean": 2.5, "ie_max": 2.5}
 
 
 def record(family: str, ours: float, ref: float, **extra) -> None:
@@ -26,14 +35,27 @@ def record(family: str, ours: float, ref: float, **extra) -> None:
         f.write(json.dumps(rec) + "\n")
 
 
-def check(family: str, ours: float, ref: float, **extra) -> None:
-    """Record, then assert ours <= F * ref + A for the family."""
-    record(family, ours, ref, **extra)
-    F, A = BARS[family]
-    assert ours <= F * ref + A, (family, float(ours), float(ref), F, A, extra)
+class Aggregate:
+    """Samples of one test: add() records and applies the per-sample guard, check() the aggregate bar."""
 
+    def __init__(self, cpu: bool = False):
+        self.cpu = cpu
+        self.sums = {}
 
-def ie_errors(e_ie, e_ref, **extra) -> None:
-    """Mean and max |IE - truth| of a grid against the reference's."""
-    check("ie_mean", float(e_ie.mean()), float(e_ref.mean()), **extra)
-    check("ie_max", float(e_ie.max()), float(e_ref.max()), **extra)
+    def add(self, family: str, ours: float, ref: float, **extra) -> None:
+        ours, ref = float(ours), float(ref)
+        record(family, ours, ref, **extra)
+        assert ours <= GUARD_F * ref + GUARD_A[family], (family, ours, ref, extra)
+        o, r, n = self.sums.get(family, (0.0, 0.0, 0))
+        self.sums[family] = (o + ours, r + ref, n + 1)
+
+    def ie_errors(self, e_ie, e_ref, **extra) -> None:
+        """Mean and max |IE - truth| of one grid against the reference's."""
+        self.add("ie_mean", e_ie.mean(), e_ref.mean(), **extra)
+        self.add("ie_max", e_ie.max(), e_ref.max(), **extra)
+
+    def check(self) -> None:
+        bars = AGG_F_CPU if self.cpu else AGG_F
+        for family, (o, r, n) in self.sums.items():
+            record(family + "_aggregate", o, r, samples=n)
+            assert o <= bars[family] * r, (family, "aggregate", o, r, n, bars[family])

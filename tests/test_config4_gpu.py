@@ -4,10 +4,9 @@ depth is irrelevant to the kernels, the widths are not) — on one rebuilt Trivi
 [0.1, 1, 1, 1, 1] re-ordered as RAG_test.py:64-107 orders them, all heads re-weighted: layers_to_be_modified = {}).
 
 Pins the automatic GQA-7 choices together at the config's shape: the 7-wave prefill workgroups (hp7, <= 2048 tokens),
-the matrix-core decode for 7-head groups and the decode step's split-K projections (the engine's rule routes long-K
-down_proj through cram_gemm_splitk, and at <= DECODE_QKV_SPLIT_MAX_ROWS rows -- this test's 2 -- q/k/v over 8 K ranges
-with the q/k/v bias added in the split-K combine), and -- with CRAM_DECODE_GEMM=all, which routes every decode
-projection through the split-K kernel -- the same for o_proj and gate/up, against
+the matrix-core decode for 7-head groups and the decode step's projections at one 128-row activation tile (this test's
+2 rows): q/k/v, o_proj and down_proj on cram_gemm_small with their K split (the q/k/v bias added in the split
+combine), and -- with CRAM_DECODE_GEMM=all -- gate/up through the split-K kernel too, against
   * the transformers drop-in on the same kernels (greedy ids up to the first near-tie, re_weighting.py:127-132);
   * the reference hook itself (oracle/hook_ref.py, dense mask, bf16 transformers) and the float32 truth (same hook
     on the float32 copy of the weights): re-weighted answer log-probs of the drop-in and of the engine within
@@ -73,11 +72,12 @@ def test_config4_engine_decode_matches_dropin(qwen7, decode_gemm, monkeypatch):
     if decode_gemm == "all":
         monkeypatch.setenv("CRAM_DECODE_GEMM", "all")
     obj, _, recs = qwen7
-    sk = DecodeSession(obj.engine, [torch.zeros(900, dtype=torch.long)] * 2, [torch.ones(1, 900, dtype=torch.float16)] * 2,
-                       {}, 4).splits_gemm
-    # the rule: down_proj (long K) always; q/k/v at <= 192 rows (one partly filled row tile); o_proj / gate/up only
-    # with CRAM_DECODE_GEMM=all
-    assert sk["qkv"] > 0 and sk["down"] > 0 and (sk["o"] > 0) == (sk["gu"] > 0) == (decode_gemm == "all"), sk
+    ds = DecodeSession(obj.engine, [torch.zeros(900, dtype=torch.long)] * 2, [torch.ones(1, 900, dtype=torch.float16)] * 2,
+                       {}, 4)
+    sk, sm = ds.splits_gemm, ds.small
+    # the rule at one 128-row activation tile (these 2 rows): q/k/v (with its bias), o_proj and down_proj on
+    # cram_gemm_small with the K split that fills the CUs; gate/up on the split-K kernel only with CRAM_DECODE_GEMM=all
+    assert sm == {"qkv": 7, "o": 8, "down": 8} and (sk["gu"] > 0) == (decode_gemm == "all"), (sk, sm)
     heads = obj.layers_to_be_modified
     qs, ps, ss = [r[0]["question"] for r in recs], [r[1] for r in recs], [r[2] for r in recs]
     batched = obj.run_RAG_batch(qs, ps, ss, max_new_tokens=16, use_graph=True)
@@ -115,6 +115,7 @@ def test_config4_answer_logprobs_match_reference_hook(qwen7):
     L, H = obj.num_hidden_layers, obj.model_num_attention_heads
     heads = {l: list(range(H)) for l in range(L)}
     eng = obj.engine
+    agg_d, agg_e = parity.Aggregate(), parity.Aggregate()
     try:
         for rec, paras, sc in recs:
             ans = rec["wrong_answer"]
@@ -131,8 +132,10 @@ def test_config4_answer_logprobs_match_reference_hook(qwen7):
             ref_err = np.abs(ref - truth).max()
             print(f"\nT={T} n={n}: |drop-in - truth| {np.abs(lp - truth).max():.4f}, |engine - truth| "
                   f"{np.abs(el - truth).max():.4f}, reference bf16 error {ref_err:.4f}")
-            parity.check("logprob_max", np.abs(lp - truth).max(), ref_err, path="drop-in")
-            parity.check("logprob_max", np.abs(el - truth).max(), ref_err, path="engine")
+            agg_d.add("logprob_max", np.abs(lp - truth).max(), ref_err, path="drop-in")
+            agg_e.add("logprob_max", np.abs(el - truth).max(), ref_err, path="engine")
+        agg_d.check()
+        agg_e.check()
     finally:
         del m16, m32
         torch.cuda.empty_cache()

@@ -1,8 +1,8 @@
 """The decode step the bench times, pinned as a whole.
 
 bench.py's decode legs run `CrAMEngine.generate` with the routing the engine picks from the batch size: config 2
-(Llama-3-8B, NQ-1000 on one GPU = two batches of 500 rows) and config 5 (20 retrieved docs, ~8.3k-token prompts, 129
-rows from the KV budget).  Kernel-level tests cover each piece against fp32; here the routed step is checked end to
+(Llama-3-8B, NQ-1000 on one GPU = two batches of 500 rows) and config 5 (20 retrieved docs, ~8.3k-token prompts, 128
+rows from the KV budget; also every GPU's share of NQ-1000 at 8 GPUs).  Kernel-level tests cover each piece against fp32; here the routed step is checked end to
 end, at Llama-3-8B's widths (D 4096, 32 / 8 heads of 128, FFN 14336, vocab 128256; two layers of random weights --
 the depth is irrelevant to the routing, the widths are not), on the bench's own inputs (rebuilt NQ prompts through the
 Llama-3 chat template, ideal scores, the nq/llama3 selected heads of layers 0-1), against
@@ -142,7 +142,7 @@ def _check_dropin(engine_rows, dropin):
 def _routing(eng, prompts, ws, heads, new):
     from cram_amd.engine import DecodeSession
     s = DecodeSession(eng, prompts, ws, heads, new)
-    r = dict(s.splits_gemm, mlp_w4=s.mlp_w4, lm_w4=s.lm_w4, attn_splits=s.splits, B=s.B)
+    r = dict(s.splits_gemm, mlp_w4=s.mlp_w4, lm_w4=s.lm_w4, attn_splits=s.splits, B=s.B, small=dict(s.small))
     del s
     return r
 
@@ -154,12 +154,13 @@ def test_config2_step_at_500_rows(l3w, monkeypatch):
     prompts, ws = _encode(tok, 500)
     new = 12
     rt = _routing(eng, prompts, ws, heads, new)
-    assert rt["mlp_w4"] and rt["lm_w4"] and rt["down"] == 8 and rt["qkv"] == 0 and rt["o"] == 0 and rt["gu"] == 0, rt
+    assert (rt["mlp_w4"] and rt["lm_w4"] and rt["down"] == 8 and rt["qkv"] == 0 and rt["o"] == 0 and rt["gu"] == 0
+            and not rt["small"]), rt
     got = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
     assert eng.generate(prompts[:3], ws[:3], heads, max_new_tokens=new, use_graph=False, stop_on_eos=False) is not None
     monkeypatch.setenv("CRAM_DECODE_GEMM", "0")
     rl = _routing(eng, prompts, ws, heads, new)
-    assert not (rl["mlp_w4"] or rl["lm_w4"] or rl["down"] or rl["qkv"] or rl["o"] or rl["gu"]), rl
+    assert not (rl["mlp_w4"] or rl["lm_w4"] or rl["down"] or rl["qkv"] or rl["o"] or rl["gu"] or rl["small"]), rl
     lib = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
     monkeypatch.delenv("CRAM_DECODE_GEMM")
     rows, frac = _compare(eng, heads, prompts, ws, got, lib, "config 2 routed vs library step")
@@ -168,16 +169,16 @@ def test_config2_step_at_500_rows(l3w, monkeypatch):
     assert _check_dropin(got, dropin) >= 6
 
 
-def test_config5_step_at_129_rows(l3w, monkeypatch):
-    """Config 5's batch (129 rows of ~8.3k tokens, the KV budget): q/k/v over 8 K ranges, down_proj over 14, lm_head
-    on gemm_w4_kernel, 2 attention splits (rows of >= 4k keys), gate/up on the library (the 4-wave kernel loses at
-    this row count)."""
+def test_config5_step_at_128_rows(l3w, monkeypatch):
+    """Config 5's batch (128 rows of ~8.3k tokens, the KV budget in whole 64-row groups): q/k/v, o_proj and down_proj
+    on cram_gemm_small with K split over 4 / 8 / 8 ranges, lm_head on gemm_w4_kernel, 2 attention splits (rows of
+    >= 4k keys), gate/up on the library (the 4-wave kernel loses at this row count)."""
     eng, tok, heads = l3w
-    prompts, ws = _encode(tok, 129, long_context=True)
+    prompts, ws = _encode(tok, 128, long_context=True)
     assert 7000 < sum(p.numel() for p in prompts) / len(prompts) < 10000
     new = 8
     rt = _routing(eng, prompts, ws, heads, new)
-    assert (rt["qkv"] == 8 and rt["down"] == 14 and rt["lm_w4"] and not rt["mlp_w4"] and rt["o"] == 0
+    assert (rt["small"] == {"qkv": 4, "o": 8, "down": 8} and rt["lm_w4"] and not rt["mlp_w4"] and rt["gu"] == 0
             and rt["attn_splits"] >= 2), rt
     got = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
     monkeypatch.setenv("CRAM_DECODE_GEMM", "0")
@@ -185,5 +186,5 @@ def test_config5_step_at_129_rows(l3w, monkeypatch):
     monkeypatch.delenv("CRAM_DECODE_GEMM")
     rows, frac = _compare(eng, heads, prompts, ws, got, lib, "config 5 routed vs library step")
     assert frac >= 0.5 and rows >= len(got) // 4
-    dropin = _dropin_ids(eng, heads, prompts, ws, [0, 128], new)
+    dropin = _dropin_ids(eng, heads, prompts, ws, [0, 127], new)
     assert _check_dropin(got, dropin) >= 4

@@ -65,13 +65,15 @@ def test_cal_logits_matches_reference(fbh, nq, kind):
     gold = [x for x in _load("tiny_ie.json.gz") if x["kind"] == kind and x["variant"] == "fp32"]
     truth = {x["idx"]: x["ie"] for x in _load("tiny_ie_f32.json.gz") if x["kind"] == kind}
     obj = fbh[kind]
+    agg = parity.Aggregate()
     for g in gold:
         rec = nq[g["idx"]]
         ie = obj.cal_logits(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
                             scores=[0, 1, 1, 1, 1], wrong_answer=rec["wrong_answer"])
         assert isinstance(ie, list) and len(ie) == obj.model_num_hidden_layers
         assert all(isinstance(v, float) for v in ie[0])
-        ie_tolerance_check(ie, g["ie"], truth[g["idx"]])
+        ie_tolerance_check(ie, g["ie"], truth[g["idx"]], agg)
+    agg.check()
 
 
 @pytest.mark.parametrize("kind", ["llama3", "qwen2"])
@@ -82,11 +84,13 @@ def test_cal_logits_bf16_logits_match_reference(fbh, nq, kind):
     truth = {x["idx"]: x["ie"] for x in _load("tiny_ie_f32.json.gz") if x["kind"] == kind}
     assert gold
     obj = fbh[kind]
+    agg = parity.Aggregate()
     for g in gold:
         rec = nq[g["idx"]]
         ie = obj.cal_logits_tensor(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
                                    scores=[0, 1, 1, 1, 1], wrong_answer=rec["wrong_answer"], round_logits=True)
-        ie_tolerance_check(ie.double().cpu().numpy(), g["ie"], truth[g["idx"]])
+        ie_tolerance_check(ie.double().cpu().numpy(), g["ie"], truth[g["idx"]], agg)
+    agg.check()
 
 
 def test_cal_logits_deterministic(fbh, nq):
@@ -261,6 +265,7 @@ def test_answer_logprobs_match_reference_hook(paths, nq, gpu_device, kind):
     truth = {(r["idx"], r["scores"], r["heads"]): np.array(r["logprobs"]) for r in rows if r["fp32"]}
     objs = {}
     worst = 0.0
+    agg = parity.Aggregate()
     for r in rows:
         if r["fp32"]:
             continue
@@ -276,9 +281,10 @@ def test_answer_logprobs_match_reference_hook(paths, nq, gpu_device, kind):
         t = truth[(r["idx"], r["scores"], r["heads"])]
         ref_err = np.abs(np.array(r["logprobs"]) - t).max()
         err = np.abs(lp.cpu().numpy() - t)
-        parity.check("logprob_max", err.max(), ref_err, kind=kind, idx=r["idx"], scores=r["scores"], heads=r["heads"])
+        agg.add("logprob_max", err.max(), ref_err, kind=kind, idx=r["idx"], scores=r["scores"], heads=r["heads"])
         worst = max(worst, err.max() / (ref_err + 1e-3))
     print(f"{kind}: worst error / reference bf16 error = {worst:.2f}")
+    agg.check()
 
 
 def test_cal_logits_batch_equals_per_question(fbh, nq):
@@ -307,6 +313,7 @@ def test_gpt2_config1_family_on_gpu(tmp_path_factory, nq, gpu_device):
     m32 = AutoModelForCausalLM.from_pretrained(path32, dtype="auto").eval()
     heads = {"0": [1], "2": [0, 3]}
     rw = Re_Weighting_Strategy(model_name=path, layers_to_be_modified=heads)
+    agg = parity.Aggregate()
     for rec in nq[:3]:
         paras = rec["ori_fake"] + rec["reranked_dense_ctxs"]
         lp = rw.answer_logprobs(question=rec["question"], paras=paras, scores=[0.1, 1, 1, 1, 1],
@@ -317,7 +324,8 @@ def test_gpt2_config1_family_on_gpu(tmp_path_factory, nq, gpu_device):
         hi = {int(k): v for k, v in heads.items()}
         truth = hook_ref.answer_logprobs(m32, ids, lw, hi, lp.size).numpy()
         ref = hook_ref.answer_logprobs(m16, ids, lw, hi, lp.size).numpy()
-        parity.check("logprob_max", np.abs(lp - truth).max(), np.abs(ref - truth).max(), kind="gpt2")
+        agg.add("logprob_max", np.abs(lp - truth).max(), np.abs(ref - truth).max(), kind="gpt2")
+    agg.check()
     out = rw.run_RAG_with_attention_weighting(question=nq[0]["question"], paras=nq[0]["ori_fake"][:1], scores=[0.1])
     assert isinstance(out, tuple) and isinstance(out[1], str)
 

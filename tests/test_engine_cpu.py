@@ -98,7 +98,7 @@ def ie_truth():
     return _gold("tiny_ie_f32.json.gz", "llama2_ie_f32.json.gz")
 
 
-def ie_tolerance_check(ie, ref, truth):
+def ie_tolerance_check(ie, ref, truth, agg=None, cpu=False):
     """Noise-floor criterion (written here once, used by the CPU and GPU suites).
 
     ref   = the reference's own bf16 (fp16 for Llama-2) run (fp32 logits), truth = the reference run on
@@ -109,7 +109,10 @@ def ie_tolerance_check(ie, ref, truth):
     """
     ie, ref, truth = (np.asarray(x, dtype=np.float64) for x in (ie, ref, truth))
     e_ref, e_ie = np.abs(ref - truth), np.abs(ie - truth)
-    parity.ie_errors(e_ie, e_ref)
+    a = agg if agg is not None else parity.Aggregate(cpu)
+    a.ie_errors(e_ie, e_ref)
+    if agg is None:                                 # a lone sample is its own aggregate
+        a.check()
     flat_t = truth.reshape(-1)
     order = np.argsort(-flat_t, kind="stable")
     sv = flat_t[order]
@@ -126,13 +129,15 @@ def test_sweep_matches_reference_ie(tiny, nq, ie_gold, ie_truth, kind):
     path, tok, model = tiny[kind]
     eng = CrAMEngine.from_hf(model)
     rows = [x for x in ie_gold if x["kind"] == kind and x["variant"] == "fp32"]
+    agg = parity.Aggregate(cpu=True)
     for g in rows[:2]:
         t = [x for x in ie_truth if x["kind"] == kind and x["idx"] == g["idx"]][0]
         ids, w = _question(tok, path, nq[g["idx"]])
         ans = torch.tensor(g["answer_ids"])
         with cpu_ops.patched_ops():
             ie = sweep.ie_question(eng, ids[0], w[0], ans).double().numpy()
-        ie_tolerance_check(ie, g["ie"], t["ie"])
+        ie_tolerance_check(ie, g["ie"], t["ie"], agg)
+    agg.check()
 
 
 def test_sweep_equals_unbatched_definition(tiny, nq):

@@ -220,11 +220,13 @@ def test_llama2_cal_logits_matches_reference(path, nq, gpu_device):
     assert obj.model.dtype == F16 and obj.engine.dtype == F16
     gold = [x for x in _load("llama2_ie.json.gz") if x["variant"] == "fp32"]
     truth = {x["idx"]: x["ie"] for x in _load("llama2_ie_f32.json.gz")}
+    agg = parity.Aggregate()
     for g in gold:
         rec = nq[g["idx"]]
         ie = obj.cal_logits(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
                             scores=[0, 1, 1, 1, 1], wrong_answer=rec["wrong_answer"])
-        ie_tolerance_check(ie, g["ie"], truth[g["idx"]])
+        ie_tolerance_check(ie, g["ie"], truth[g["idx"]], agg)
+    agg.check()
 
 
 @pytest.mark.parametrize("case", [0, 1])
@@ -263,6 +265,7 @@ def test_llama2_logprobs_match_reference_hook(path, nq, gpu_device):
     rows = _load("llama2_logprobs.json.gz")
     truth = {(r["idx"], r["scores"], r["heads"]): np.array(r["logprobs"]) for r in rows if r["fp32"]}
     objs = {}
+    agg = parity.Aggregate()
     for r in rows:
         if r["fp32"]:
             continue
@@ -276,8 +279,9 @@ def test_llama2_logprobs_match_reference_hook(path, nq, gpu_device):
         t = truth[(r["idx"], r["scores"], r["heads"])]
         ref_err = np.abs(np.array(r["logprobs"]) - t).max()
         err = np.abs(lp.cpu().numpy() - t)
-        parity.check("logprob_max", err.max(), ref_err, kind="llama2", idx=r["idx"], scores=r["scores"],
-                     heads=r["heads"])
+        agg.add("logprob_max", err.max(), ref_err, kind="llama2", idx=r["idx"], scores=r["scores"],
+                heads=r["heads"])
+    agg.check()
 
 
 def test_llama2_engine_batched_decode(path, nq, gpu_device):

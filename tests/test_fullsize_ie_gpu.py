@@ -112,7 +112,9 @@ def test_sweep_ie_matches_fp32_truth_at_llama3_8b_shape(setup):
     assert torch.isfinite(ours).all()
     e_hook = (hook - truth).abs()
     # values: no further from the float32 truth than the reference algorithm's own bf16 run (DESIGN.md §3 bar)
-    parity.ie_errors(e_ours, e_hook, shape="llama3-8b")
+    agg = parity.Aggregate()                        # one grid: its own aggregate
+    agg.ie_errors(e_ours, e_hook, shape="llama3-8b")
+    agg.check()
     # ranking: the top-k sets recover the truth's at least as well as the reference's bf16 run does
     for k in (1, 2, 4, 8, 16, 32):
         ko, kh = _topk_overlap(ours, truth, k), _topk_overlap(hook, truth, k)

@@ -41,6 +41,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3")
     ap.add_argument("--M", type=int, default=256)
+    ap.add_argument("--hot", action="store_true", help="one weight copy (Infinity-Cache resident) instead of cycling")
+    ap.add_argument("--only", default="", help="comma list of shapes")
     args = ap.parse_args()
     sp = ModelSpec.llama3_8b() if args.model == "llama3" else ModelSpec.qwen2_7b()
     dev = torch.device("cuda:0")
@@ -52,7 +54,9 @@ def main():
     ws = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
     for name, (N, K) in shapes.items():
         wbytes = N * K * 2
-        n_copies = max(2, min(16, -(-(640 << 20) // wbytes)))
+        if args.only and name not in args.only.split(","):
+            continue
+        n_copies = 1 if args.hot else max(2, min(16, -(-(640 << 20) // wbytes)))
         ws_ = [(torch.randn(N, K, generator=g, device=dev) * 0.02).to(torch.bfloat16) for _ in range(n_copies)]
         x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
         ref = (x.float() @ ws_[0].float().t())
