@@ -277,7 +277,7 @@ def main():
         for T, n_ans, w, layers in mine:
             p0 = int((w.view(-1) != 1).nonzero()[0, 0]) if bool((w != 1).any()) else T
             p0 = 0 if args.no_prefix_skip else p0
-            flops += sweep.sweep_flops(spec, T, n_ans, p0, layers)
+            flops += sweep.sweep_flops(spec, T, n_ans, p0, layers, base_variant=not sweep.row_exact(eng))
         ksum = ops.TIMER.summary()
         kt = ksum.get("cram_prefill", None)
         # the projections: cram_gemm (gemm_w4_kernel, every epilogue), its split-K tail, and F.linear calls left
@@ -428,7 +428,7 @@ def main():
         if want_ie:
             qi, ids, w, ans = ie["work"][0]
             units_s = cpu_baseline.sample_units(L, H, max(1, args.cpu_units))
-            r = cpu_baseline.time_ie_units(cpu_model, ids.cpu(), w, ans.cpu(), units_s)
+            r = cpu_baseline.time_ie_units(cpu_model, ids.cpu(), w, ans.cpu(), units_s, log=log)
             sp_ = r["spread"]
             lay_s = sorted(set(l for l, _ in units_s))
             cpu = {"value": r["units_per_s"], "unit": "heads/s", "cores": r["cores"], "kind": "port",

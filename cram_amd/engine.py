@@ -159,6 +159,11 @@ class CrAMEngine:
         self.device = embed.device
         self.dtype = embed.dtype
         self.scale = spec.head_dim ** -0.5
+        # the IE sweep's row-exact modes (sweep.py): fused_any_rows puts every projection on the 4-wave kernel
+        # whatever the row count; no_tail_split (the baseline forward) keeps every row of a launch on it too, so a
+        # row computes the same bits there as in the whole waves of any variant batch
+        self.fused_any_rows = False
+        self.no_tail_split = False
         if self.device.type == "cuda":
             gemm_tune.ensure()          # pinned q/k/v and o_proj GEMM solutions, used inside gemm_tune.pinned()
 
@@ -275,7 +280,8 @@ class CrAMEngine:
             return False
         D, F = self.spec.hidden, self.spec.intermediate
         M = x.numel() // x.shape[-1]
-        return M >= self.FUSED_MLP_MIN_ROWS and (2 * F) % 256 == 0 and D % 64 == 0 and D >= 128
+        return ((M >= self.FUSED_MLP_MIN_ROWS or self.fused_any_rows) and (2 * F) % 256 == 0 and D % 64 == 0
+                and D >= 128)
 
     def _gemm_residual(self, x: torch.Tensor, w: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
         """h + x @ w^T on row buffers with the add in the GEMM epilogue.  The 4-wave kernel runs one 256 x 256 tile
@@ -284,6 +290,8 @@ class CrAMEngine:
         the K) then leave ~7/8 of the chip idle for a whole tile time.  Rows past the last whole wave go instead
         through the split-K form with the same epilogue, their K cut into ranges until the tail fills the chip."""
         M, K, N = x.numel() // x.shape[-1], x.shape[-1], w.shape[0]
+        if self.no_tail_split:                 # one kernel for every row
+            return ops.gemm(x, w, residual=h)
         ntn, mt = N // 256, -(-M // 256)
         waves = mt * ntn // self.num_cus
         mt_main = waves * self.num_cus // ntn

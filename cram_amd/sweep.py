@@ -17,16 +17,21 @@ Here, per question:
   4. answer logits come from the fp32 gather-dot kernel (no full vocab);
   5. IE stays on the device; one host copy per question (or one all-gather).
 Noise cancellation: in the reference, ori and cur share bit-identical arithmetic
-for every layer below the hooked one (re_weighting.py:159 vs :169).  Here each
-layer's batch also carries one UN-perturbed variant, and IE[l, h] = sum over the
-un-perturbed row - sum over variant h, so the two sides again share their
-rounding everywhere except in the perturbed computation (the layer-l batch
-shape differs from the batch-1 baseline, so re-using the baseline's ori would
-leave uncorrelated bf16 rounding in the difference).
+for every layer below the hooked one (re_weighting.py:159 vs :169).  Here the
+same holds by construction (row-exact mode): the baseline forward
+runs every projection on the kernels the variant batches run (the 4-wave GEMM
+whatever the row count, no split-K tail), its attention over the suffix rows
+[p0, T) as one call of the shape the variants' calls have, so an un-perturbed
+row computes the same bits in the baseline as in any variant batch, and
+IE[l, h] = ori(baseline) - sum over variant h.  Where that cannot hold (a model
+whose widths keep it off the fused kernels, the CPU stand-ins) each layer's batch
+carries one extra, un-perturbed variant and IE[l, h] = its sum - variant h's.
 Work per question: L*H*(L-1)/2 + ... layer-forwards instead of (1 + L*H) * L.
 """
 from __future__ import annotations
 
+import contextlib
+import os
 from typing import Optional
 
 import torch
@@ -34,6 +39,9 @@ import torch
 from . import gemm_tune, ops
 from .bias import CredibilityBias
 from .engine import CrAMEngine, padded_rows
+
+# drop the un-perturbed variant where the arithmetic is row-exact (CRAM_SWEEP_ROW_EXACT=0 keeps it: A/B, tests)
+ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "1") != "0"
 
 
 class QuestionCache:
@@ -44,35 +52,81 @@ class QuestionCache:
         self.q = []        # roped q      [1, T, Hq, d]
         self.k = []        # roped k      [1, T, Hkv, d]
         self.v = []        # v            [1, T, Hkv, d]
-        self.a = []        # un-biased attention output [1, T, Hq, d]
+        self.a = []        # un-biased attention output [1, T, Hq, d] (last layer, row-exact: the last n rows)
+        self.exact = False  # built row-exact (baseline()): the sweep needs no un-perturbed variant
+
+
+def row_exact(eng: CrAMEngine) -> bool:
+    """True when the sweep's un-perturbed rows compute the same bits in the baseline forward as in the variant
+    batches (every projection on the fused 4-wave kernels: a CUDA engine at 16-bit widths the fused epilogues
+    take); the sweep then drops the per-layer un-perturbed variant."""
+    if not ROW_EXACT or eng.device.type != "cuda":
+        return False
+    x = torch.empty((1, eng.spec.hidden), device="meta")
+    with _modes(eng, True, False):
+        return eng._fused_residual_ok(x) and eng._fused_qkv_ok(x, eng.layers[0])
+
+
+@contextlib.contextmanager
+def _modes(eng: CrAMEngine, fused_any_rows: bool, no_tail_split: bool):
+    prev = eng.fused_any_rows, eng.no_tail_split
+    eng.fused_any_rows, eng.no_tail_split = fused_any_rows, no_tail_split
+    try:
+        yield
+    finally:
+        eng.fused_any_rows, eng.no_tail_split = prev
 
 
 @torch.no_grad()
-def baseline(eng: CrAMEngine, ids: torch.Tensor, n_ans: int, keep: bool = True):
-    """Un-hooked forward; returns (final hidden of the last n rows [n, D], QuestionCache)."""
+def baseline(eng: CrAMEngine, ids: torch.Tensor, n_ans: int, keep: bool = True, p0: int = 0):
+    """Un-hooked forward; returns (final hidden of the last n rows [n, D], QuestionCache).
+
+    Row-exact (row_exact(eng)): the fused projections at any row count, and each layer's attention as two calls,
+    rows [0, p0) and rows [p0, T) (the last layer: the last n rows) -- the query blocks of the variants' calls."""
     sp = eng.spec
     T = ids.shape[-1]
     cos, sin = eng.rope_tables(T)
     h = eng.embed[ids.view(1, T)]
     qc = QuestionCache()
     L = sp.num_layers
-    for l in range(L):
-        lw = eng.layers[l]
-        x = eng.rmsnorm(h, lw.ln1)
-        q, k, v = eng.qkv(x, lw, cos, sin)
-        a = eng.attention(q, k, v)
-        if keep:
-            qc.h_in.append(h)
-            qc.q.append(q)
-            qc.k.append(k)
-            qc.v.append(v)
-            qc.a.append(a)
-        if l == L - 1:
-            a = a[:, -n_ans:]
-            h = h[:, -n_ans:]
-        h, x2 = eng.add_rmsnorm(ops.linear(a.flatten(-2), lw.wo), h, lw.ln2)
-        h = h + eng.mlp(x2, lw)
-    return eng.rmsnorm(h, eng.norm)[0], qc
+    exact = row_exact(eng)
+    p0 = max(0, min(int(p0), T - n_ans))
+    with _modes(eng, exact, exact):
+        for l in range(L):
+            lw = eng.layers[l]
+            x = eng.rmsnorm(h, lw.ln1)
+            q, k, v = eng.qkv(x, lw, cos, sin)
+            last = l == L - 1
+            if not exact:
+                a = eng.attention(q, k, v)
+            elif last:
+                a = eng.attention(q[:, -n_ans:], k, v)
+            else:
+                a = torch.empty((1, T, sp.num_heads, sp.head_dim), dtype=eng.dtype, device=eng.device)
+                if p0 > 0:
+                    ops.attn_prefill(q[:, :p0].transpose(1, 2), k[:, :p0].transpose(1, 2), v[:, :p0].transpose(1, 2),
+                                     scale=eng.scale, out=a[:, :p0])
+                ops.attn_prefill(q[:, p0:].transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=eng.scale,
+                                 out=a[:, p0:])
+            if keep:
+                qc.h_in.append(h)
+                qc.q.append(q)
+                qc.k.append(k)
+                qc.v.append(v)
+                qc.a.append(a)
+            if last:
+                a = a[:, -n_ans:]
+                h = h[:, -n_ans:]
+            if exact:
+                rows = a.shape[1]
+                h2, x2 = eng.o_proj_norm(a.reshape(rows, sp.q_size), lw, h.reshape(rows, sp.hidden))
+                h, _ = eng.mlp_residual(x2, lw, h2)
+                h = h.view(1, rows, sp.hidden)
+            else:
+                h, x2 = eng.add_rmsnorm(ops.linear(a.flatten(-2), lw.wo), h, lw.ln2)
+                h = h + eng.mlp(x2, lw)
+        qc.exact = exact
+        return eng.rmsnorm(h, eng.norm)[0], qc
 
 
 def first_biased_row(bias: torch.Tensor, W: int) -> int:
@@ -85,14 +139,19 @@ def first_biased_row(bias: torch.Tensor, W: int) -> int:
 
 @torch.no_grad()
 def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tensor, W: int, n_ans: int,
-                   heads: Optional[torch.Tensor] = None, p0: int = 0) -> torch.Tensor:
-    """Final hidden states [H'+1, n, D]: variants 'head heads[i] of layer l re-weighted', then the un-perturbed one.
+                   heads: Optional[torch.Tensor] = None, p0: int = 0, with_base: Optional[bool] = None):
+    """Final hidden states [(1 +) H', n, D]: (with_base; default: when the cache is not row-exact) the un-perturbed
+    variant first, then the variants 'head heads[i] of layer l re-weighted'.  The un-perturbed variant leads so that
+    its rows sit in the whole waves of every projection launch, away from the split-K tail (engine._gemm_residual).
 
     Rows < p0 (before the first biased key) are taken from the baseline instead of being recomputed per variant."""
     sp = eng.spec
     H = sp.num_heads
     heads = torch.arange(H, device=eng.device) if heads is None else heads
-    Hv = heads.numel() + 1                                               # + the un-perturbed variant (last)
+    if with_base is None:
+        with_base = not qc.exact
+    b0 = 1 if with_base else 0
+    Hv = heads.numel() + b0                                             # (+ the un-perturbed variant, first)
     T_full = qc.h_in[l].shape[1]
     L = sp.num_layers
     last = l == L - 1
@@ -109,19 +168,20 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     abuf = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=eng.device)
     x = abuf[:M].view(Hv, rows, H, sp.head_dim)
     x.copy_(a_base.expand(Hv, rows, H, sp.head_dim))                    # [Hv, rows, Hq, d]
-    idx = torch.arange(Hv - 1, device=eng.device)
-    x[idx, :, heads] = a_bias[0].permute(1, 0, 2)[heads]                # variant i <- biased head heads[i]
+    idx = torch.arange(b0, Hv, device=eng.device)
+    x[idx, :, heads] = a_bias[0].permute(1, 0, 2)[heads]                # variant b0 + i <- biased head heads[i]
     lw = eng.layers[l]
     hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
     hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
-    h, x2 = eng.o_proj_norm(abuf, lw, hin)                             # [Mp, D]
-    h, m = eng.mlp_residual(x2, lw, h)                                  # layer output h (+ m when deferred)
-    if not last:
-        cos, sin = eng.rope_tables(T_full)
-        for l2 in range(l + 1, L):
-            pre = None if p0 == 0 else (qc.k[l2][:, :p0], qc.v[l2][:, :p0])         # suffix row t at p0 + t
-            h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m,
-                                  prefix=pre)
+    with _modes(eng, qc.exact, False):
+        h, x2 = eng.o_proj_norm(abuf, lw, hin)                         # [Mp, D]
+        h, m = eng.mlp_residual(x2, lw, h)                              # layer output h (+ m when deferred)
+        if not last:
+            cos, sin = eng.rope_tables(T_full)
+            for l2 in range(l + 1, L):
+                pre = None if p0 == 0 else (qc.k[l2][:, :p0], qc.v[l2][:, :p0])     # suffix row t at p0 + t
+                h, m = eng.layer_rows(h, Hv, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m,
+                                      prefix=pre)
     rows = Hv * n_ans
     if m is None:
         y = ops.rmsnorm(h[:rows], eng.norm, sp.eps)
@@ -142,6 +202,15 @@ def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answ
         return _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_prefix)
 
 
+def _answer_sums(lg: torch.Tensor) -> torch.Tensor:
+    """Row sums of [R, n] answer logits, left to right: the same fp32 additions whatever R (a reduction kernel's
+    order may depend on the tensor's shape, and ori and cur must round alike)."""
+    s = lg[:, 0].clone()
+    for j in range(1, lg.shape[1]):
+        s += lg[:, j]
+    return s
+
+
 def _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_prefix):
     sp = eng.spec
     dev = eng.device
@@ -149,23 +218,27 @@ def _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_pref
     n = int(answer_ids.numel())
     ans = answer_ids.to(dev, torch.int32).view(-1)
     cb = CredibilityBias.build([weight16.view(1, -1)], {}, sp.num_layers, sp.num_heads, dev, eng.dtype)
-    _, qc = baseline(eng, ids, n)
+    p0 = first_biased_row(cb.bias, cb.W) if skip_prefix else 0
+    hf, qc = baseline(eng, ids, n, p0=p0)
     layers = range(sp.num_layers) if layers is None else layers
     out = torch.empty((len(layers), sp.num_heads), dtype=torch.float32, device=dev)
-    H1 = sp.num_heads + 1
-    ans_rep = ans.repeat(H1)
-    p0 = first_biased_row(cb.bias, cb.W) if skip_prefix else 0
+    H = sp.num_heads
+    Hv = H if qc.exact else H + 1
+    ans_rep = ans.repeat(Hv)
+    ori = _answer_sums(eng.answer_logits(hf, ans, round_logits).view(1, n))[0] if qc.exact else None
     for i, l in enumerate(layers):
-        hv = layer_variants(eng, qc, l, cb.bias, cb.W, n, p0=p0)       # [H+1, n, D]
-        sums = eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_logits).view(H1, n).sum(1)
-        out[i] = sums[-1] - sums[:-1]                                   # ori - cur
+        hv = layer_variants(eng, qc, l, cb.bias, cb.W, n, p0=p0)       # [Hv, n, D]
+        sums = _answer_sums(eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_logits).view(Hv, n))
+        out[i] = ori - sums if qc.exact else sums[0] - sums[1:]        # ori - cur
     return out
 
 
-def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None) -> float:
+def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None, base_variant: bool = False) -> float:
     """Algorithmic GEMM+attention flops of ie_question(layers=...) (for roofline accounting): one baseline
-    forward plus the suffix work of every swept layer; p0 = skipped prefix rows."""
+    forward plus the suffix work of every swept layer; p0 = skipped prefix rows; base_variant: the batches carry
+    the un-perturbed variant (not row-exact)."""
     L, H, d, D = spec.num_layers, spec.num_heads, spec.head_dim, spec.hidden
+    Hv = H + 1 if base_variant else H
 
     def attn(tq, s):   # tq queries at positions s-tq .. s-1, causal
         vis = tq * (s - tq) + tq * (tq + 1) / 2.0
@@ -183,10 +256,10 @@ def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None) -> float:
         last = l == L - 1
         rows = n_ans if last else Ts
         f += attn(rows, T)                                              # all-heads biased attention
-        f += (H + 1) * (1 - qkv_frac) * lay(rows)                       # o_proj + MLP of layer l, H+1 variants
+        f += Hv * (1 - qkv_frac) * lay(rows)                            # o_proj + MLP of layer l, Hv variants
         for l2 in range(l + 1, L):
             if l2 == L - 1:
-                f += (H + 1) * (qkv_frac * lay(Ts) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T))
+                f += Hv * (qkv_frac * lay(Ts) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T))
             else:
-                f += (H + 1) * (lay(Ts) + attn(Ts, T))
+                f += Hv * (lay(Ts) + attn(Ts, T))
     return f

@@ -83,8 +83,9 @@ def cores() -> int:
 
 
 @torch.no_grad()
-def time_ie_units(model, ids: torch.Tensor, w16: torch.Tensor, answer_ids: torch.Tensor, units) -> dict:
-    """Reference-algorithm IE units on the CPU: one hooked full forward + .item() per (layer, head)."""
+def time_ie_units(model, ids: torch.Tensor, w16: torch.Tensor, answer_ids: torch.Tensor, units, log=None) -> dict:
+    """Reference-algorithm IE units on the CPU: one hooked full forward + .item() per (layer, head).  log: called
+    with a progress line every 8 units (the bench's stderr: a silent minute reads as a hang on the GPU box)."""
     torch.set_num_threads(cores())
     lw = hook_ref.log_weight(w16.reshape(1, -1).cpu())
     ids = ids.reshape(1, -1).cpu()
@@ -102,6 +103,8 @@ def time_ie_units(model, ids: torch.Tensor, w16: torch.Tensor, answer_ids: torch
                 x.remove()
         vals.append((ori - cur).item())
         per.append(time.perf_counter() - t1)
+        if log is not None and len(per) % 8 == 0:
+            log(f"cpu IE sample: {len(per)}/{len(units)} units at {time.perf_counter() - t0:.1f}s")
     dt = time.perf_counter() - t0
     srt = sorted(per)
     return {"units": len(units), "seconds": dt, "units_per_s": len(units) / dt, "cores": cores(),
