@@ -149,7 +149,7 @@ def fp32_lm_head(model):
     return model.lm_head.register_forward_hook(hook)
 
 
-def gen_ie(rw, kinds=(("llama3", 6), ("qwen2", 3)), out="tiny_ie.json.gz"):
+def gen_ie(rw, kinds=(("llama3", 6), ("qwen2", 8)), out="tiny_ie.json.gz"):
     res = []
     for kind, nq in kinds:
         path = tm.save_model(kind, MODEL_ROOT)
@@ -178,7 +178,7 @@ def gen_ie(rw, kinds=(("llama3", 6), ("qwen2", 3)), out="tiny_ie.json.gz"):
         json.dump(res, f)
 
 
-def gen_ie_f32(rw, kinds=(("llama3", 6), ("qwen2", 3)), out="tiny_ie_f32.json.gz"):
+def gen_ie_f32(rw, kinds=(("llama3", 6), ("qwen2", 8)), out="tiny_ie_f32.json.gz"):
     """The reference's cal_logits on the float32 copy of the tiny models: the IE ground truth."""
     res = []
     for kind, nq in kinds:

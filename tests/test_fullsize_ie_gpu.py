@@ -39,7 +39,7 @@ def setup():
     eng = CrAMEngine.random(ModelSpec.llama3_8b(), dev, seed=1234, rope_theta=500000.0)
     tok = AutoTokenizer.from_pretrained(os.path.join(REPO, "data", "tok_llama3"))
     data = json.load(gzip.open(os.path.join(REPO, "data", "nq_1000.json.gz"), "rt", encoding="utf-8"))
-    rec = data[3]
+    rec = data[int(os.environ.get("CRAM_FULLSIZE_Q", 3))]          # another question only for diagnostics
     _, enc, w, _ = spans.encode(tok, "Meta-Llama-3-8B-Instruct", rec["question"],
                                 rec["ori_fake"] + rec["reranked_dense_ctxs"], [0, 1, 1, 1, 1], rec["wrong_answer"])
     ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]

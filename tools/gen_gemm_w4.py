@@ -101,7 +101,28 @@ VENDOR = dict(
     NEXT_X0=[105, 106, 109, 112, 114, 117, 120, 123],
     LGKM_END=126)
 # (variant B: every piece of tile t + 2 before B3 -- measured 0.95-0.97x of A, r04; dropped)
-VARIANTS = {"A": VENDOR}
+# Round 5 probes (same-process A/B on the sweep's five GEMMs, tools/ab_gemm_builds.py, profiles/r05/ab_loop/; every
+# output bit-equal): C 0.92-0.96x, D 0.99-1.00x, E 0.92-0.97x of A -- the vendor placement stays.
+# variant C (r05 probe): one rendezvous for both operands' k-step 1 fragments (B12) instead of B1 + B2 -- every wave
+# has read all of stage s once its 16 k-step 1 fragments have landed, so both DMA groups of tile t + 2 may follow
+TWO_BARRIER = dict(
+    Y1=[0, 2, 4, 6, 8, 10, 12, 14],
+    X1=[16, 18, 20, 22, 24, 26, 28, 30],
+    B12=(40, 41),
+    YDMA=[42, 43, 46, 49, 52, 55, 58, 61, 64, 66],
+    XDMA=[67, 68, 71, 74, 77, 80, 96, 100, 124, 125],
+    LATE=3,
+    TOGGLE=[83, 84],
+    B3=(91, 92),
+    NEXT_Y0=[93, 94, 95, 97, 98, 102, 103, 104],
+    NEXT_X0=[105, 106, 109, 112, 114, 117, 120, 123],
+    LGKM_END=126)
+# variants D / E (r05 probe): the wait closing a tile counts (lgkmcnt(3)): the next tile's last three weight fragments
+# (first used by MFMA 40) may still be landing while its first MFMAs issue; the k-step 1 rendezvous (<= gap 39) or,
+# without DMA, an extra wait at gap 20 drains them
+VAR_D = dict(VENDOR, LGKM_END_N=3, CARRY_WAIT=20)
+VAR_E = dict(TWO_BARRIER, B12=(38, 39), LGKM_END_N=3, CARRY_WAIT=20)
+VARIANTS = {"A": VENDOR}           # (+ "C": TWO_BARRIER, "D": VAR_D, "E": VAR_E to rebuild the probes)
 
 
 # Diagnostic stamps (variant "S", -DCRAM_W4_STAMPS builds only): s_memtime brackets around each rendezvous, the
@@ -126,15 +147,22 @@ def body(dma_on: bool, next_on: bool, c=VENDOR, stamps=False):
 
     place(c["Y1"], [[read("y", 1, f)] for f in range(8)])
     place(c["X1"], [[read("x", 1, f)] for f in range(8)])
-    if dma_on:
+    if dma_on and "B12" in c:
+        gaps[c["B12"][0]] += (stamp_open() if stamps else []) + ["s_waitcnt lgkmcnt(0)"]
+        gaps[c["B12"][1]] += ["s_barrier"] + (stamp_close(80) if stamps else [])
+        place_dma(gaps, c["YDMA"], "y")
+        place_dma(gaps, c["XDMA"], "x")
+    elif dma_on:
         gaps[c["B1"][0]] += (stamp_open() if stamps else []) + ["s_waitcnt lgkmcnt(0)"]
         gaps[c["B1"][1]] += ["s_barrier"] + (stamp_close(80) if stamps else [])
         place_dma(gaps, c["YDMA"], "y")
         gaps[c["B2"][0]] += (stamp_open() if stamps else []) + ["s_waitcnt lgkmcnt(0)"]
         gaps[c["B2"][1]] += ["s_barrier"] + (stamp_close(81) if stamps else [])
         place_dma(gaps, c["XDMA"], "x")
-    else:
-        gaps[c["B2"][0]].append("s_waitcnt lgkmcnt(0)")    # k-step 1's fragments land before its MFMAs
+    else:                                                   # k-step 1's fragments land before its MFMAs
+        if c.get("CARRY_WAIT") is not None:
+            gaps[c["CARRY_WAIT"]].append("s_waitcnt lgkmcnt(0)")
+        gaps[(c["B12"] if "B12" in c else c["B2"])[0]].append("s_waitcnt lgkmcnt(0)")
     if next_on:
         toggle = ["v_xor_b32 %[rx0], 0x10000, %[rx0]", "v_xor_b32 %[ry0], 0x10000, %[ry0]",
                   "v_xor_b32 %[rx1], 0x10000, %[rx1]", "v_xor_b32 %[ry1], 0x10000, %[ry1]"]
@@ -146,7 +174,7 @@ def body(dma_on: bool, next_on: bool, c=VENDOR, stamps=False):
         gaps[c["B3"][1]] += ["s_barrier"] + (stamp_close(82) if stamps else [])
         place(c["NEXT_Y0"], [[read("y", 0, f)] for f in range(8)])
         place(c["NEXT_X0"], [[read("x", 0, f)] for f in range(8)])
-        gaps[c["LGKM_END"]].append("s_waitcnt lgkmcnt(0)")
+        gaps[c["LGKM_END"]].append(f"s_waitcnt lgkmcnt({c.get('LGKM_END_N', 0)})")
     lines = []
     if stamps and dma_on:                        # whole-tile time: the bracket closes after the last MFMA
         lines += ["s_memtime s[92:93]"]
