@@ -86,7 +86,8 @@ def decode_leg_roofline(spec, phases, dtype):
     over the timed repeats:
       prefill  MFMA-bound: algorithmic FLOPs of the packed prefill — per prompt of T tokens, every layer's
                projections 2 * params * T (ModelSpec.layer_flops) + causal attention 4 * d * Hq * T(T+1)/2, and the
-               lm_head of the last row 2 * D * V — over the prefill's time, against the dense bf16 peak;
+               lm_head of the last row 2 * D * V — over the prefill's time, against the dense bf16 peak; the rows of
+               the batch's shared prefix (DecodeSession.shared_prefix, computed once) are counted once;
       steps    HBM-bound: per greedy step, every weight once (L layers' projections + lm_head, the embedding is a
                B-row gather) + every row's visible K and V (L * Hkv * d * 2 tensors * 2 B per key, the keys growing
                by one per step) over the steps' time, against 8 TB/s (6.3 achievable)."""
@@ -100,8 +101,12 @@ def decode_leg_roofline(spec, phases, dtype):
     n_steps = 0
     for ph in phases:
         lens = ph["lens"]
+        p = ph.get("prefix", 0)
+        att = lambda T: L * 4.0 * spec.head_dim * spec.num_heads * T * (T + 1) / 2
+        if p:
+            pf_flops += L * spec.layer_flops(p) + att(p)
         for T in lens:
-            pf_flops += L * spec.layer_flops(T) + L * 4.0 * spec.head_dim * spec.num_heads * T * (T + 1) / 2 + 2.0 * D * V
+            pf_flops += L * spec.layer_flops(T - p) + att(T) - att(p) + 2.0 * D * V
         pf_ms += ph["t0"].elapsed_time(ph["prefill"])
         cap_ms += ph["prefill"].elapsed_time(ph["capture"])
         st_ms += ph["capture"].elapsed_time(ph["steps"])

@@ -17,7 +17,7 @@ _c_int32_p = POINTER(ctypes.c_int32)
 _c_uint8_p = POINTER(ctypes.c_uint8)
 _c_float_p = POINTER(c_float)
 
-ABI_VERSION = 6   # CRAM_ABI_VERSION of include/cram_attn.h
+ABI_VERSION = 7   # CRAM_ABI_VERSION of include/cram_attn.h
 
 # name -> (restype, argtypes); the exact export list of include/cram_attn.h
 SIGNATURES = {
@@ -37,6 +37,11 @@ SIGNATURES = {
     "cram_attn_prefill_varlen": (c_int, [
         c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64,
         c_void_p, c_int64, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float,
+        c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p,
+    ]),
+    "cram_attn_prefill_varlen_cached": (c_int, [
+        c_void_p, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64, c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
         c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_void_p,
     ]),
     "cram_attn_decode_workspace_size": (c_size_t, [c_int, c_int, c_int, c_int]),

@@ -221,6 +221,8 @@ struct PrefillParams {
   int nqb, nblocks;
   int hp;             // query heads per workgroup (1, 2 or 4; divides the GQA group)
   const int32_t* cu;  // varlen: [B+1] token offsets of packed sequences (q/k/v/o batch strides unused)
+  int kv_cache;       // varlen with cached keys: sequence b's keys are rows 0 .. q_pos0 + Tq_b - 1 of k + b k_sb
+                      // (a shared prefix of q_pos0 rows, then its own rows); its queries sit at q_pos0 + i
 };
 
 template <int D, int BK_ = 64>
@@ -266,11 +268,13 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
 
   // per-sequence extent: uniform batch, or packed varlen sequences (cu_seqlens)
   int Tq = p.Tq, S = p.S, q_pos0 = p.q_pos0;
-  int64_t tok0 = 0;
+  int64_t tok0 = 0, ktok0 = 0;
   if (p.cu) {
     tok0 = p.cu[b];
-    Tq = S = p.cu[b + 1] - (int)tok0;
-    q_pos0 = 0;
+    Tq = p.cu[b + 1] - (int)tok0;
+    q_pos0 = p.kv_cache ? p.q_pos0 : 0;
+    S = q_pos0 + Tq;
+    ktok0 = p.kv_cache ? 0 : tok0;
     if (qblk * BQ >= Tq) return;   // whole workgroup exits before any barrier
   }
   const int tid = threadIdx.x, lane = tid & 63;
@@ -282,8 +286,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void prefill_kernel(PrefillParams p) 
   const int qpos = q_pos0 + qrow;
 
   const T* qb = static_cast<const T*>(p.q) + b * p.q_sb + tok0 * p.q_st + hq * p.q_sh;
-  const T* kbase = static_cast<const T*>(p.k) + b * p.k_sb + tok0 * p.k_st + hkv * p.k_sh;
-  const T* vbase = static_cast<const T*>(p.v) + b * p.v_sb + tok0 * p.v_st + hkv * p.v_sh;
+  const T* kbase = static_cast<const T*>(p.k) + b * p.k_sb + ktok0 * p.k_st + hkv * p.k_sh;
+  const T* vbase = static_cast<const T*>(p.v) + b * p.v_sb + ktok0 * p.v_st + hkv * p.v_sh;
   // per-wave head enable; the workgroup stages the bias tile if any of its heads is enabled
   const bool has_bias = (p.bias != nullptr) && (p.enable != nullptr);
   const bool en = has_bias && p.enable[b * p.en_sb + hq] != 0;
@@ -1228,7 +1232,7 @@ int cram_attn_prefill(const void* q, int64_t q_sb, int64_t q_sh, int64_t q_st, c
   p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = Tq; p.S = S; p.W = bias ? W : 0; p.q_pos0 = q_pos0;
   p.scale_log2 = scale * kLog2e;
-  p.cu = nullptr;
+  p.cu = nullptr; p.kv_cache = 0;
   return dispatch_prefill(p, d, dtype, (hipStream_t)stream);
 }
 
@@ -1255,7 +1259,38 @@ int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const vo
   p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = max_len; p.S = max_len; p.W = bias ? W : 0; p.q_pos0 = 0;
   p.scale_log2 = scale * kLog2e;
-  p.cu = cu_seqlens;
+  p.cu = cu_seqlens; p.kv_cache = 0;
+  return dispatch_prefill(p, d, dtype, (hipStream_t)stream);
+}
+
+int cram_attn_prefill_varlen_cached(const void* q, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sb,
+                                    int64_t k_sh, int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh,
+                                    int64_t v_st, void* o, int64_t o_sh, int64_t o_st, const int32_t* cu_seqlens,
+                                    int B, int max_len, int prefix, int Hq, int Hkv, int d, float scale,
+                                    const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                                    int dtype, cram_stream_t stream) {
+  if (!q || !k || !v || !o || !cu_seqlens) return CRAM_ERR_INVALID_ARG;
+  if (B <= 0 || Hq <= 0 || Hkv <= 0 || max_len <= 0 || prefix < 0 || Hq % Hkv != 0 || k_sb < 0 || v_sb < 0)
+    return CRAM_ERR_INVALID_ARG;
+  if ((d != 64 && d != 128) || !dtype_ok(dtype)) return CRAM_ERR_UNSUPPORTED;
+  if (!al16(q) || !al16(k) || !al16(v) || !al16(o)) return CRAM_ERR_ALIGNMENT;
+  if (!m8(q_sh) || !m8(q_st) || !m8(k_sb) || !m8(k_sh) || !m8(k_st) || !m8(v_sb) || !m8(v_sh) || !m8(v_st) ||
+      !m8(o_sh) || !m8(o_st))
+    return CRAM_ERR_ALIGNMENT;
+  if (bias && W < 0) return CRAM_ERR_INVALID_ARG;
+  if ((int64_t)(prefix + max_len) * (k_st > v_st ? k_st : v_st) * 2 + 2 * d >= (1ll << 31) ||
+      (int64_t)W * 4 >= (1ll << 31))
+    return CRAM_ERR_UNSUPPORTED;
+  PrefillParams p;
+  p.q = q; p.q_sb = 0; p.q_sh = q_sh; p.q_st = q_st;
+  p.k = k; p.k_sb = k_sb; p.k_sh = k_sh; p.k_st = k_st;
+  p.v = v; p.v_sb = v_sb; p.v_sh = v_sh; p.v_st = v_st;
+  p.o = o; p.o_sb = 0; p.o_sh = o_sh; p.o_st = o_st;
+  p.bias = (bias && enable) ? bias : nullptr; p.bias_sb = bias_sb;
+  p.enable = (bias && enable) ? enable : nullptr; p.en_sb = en_sb;
+  p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.Tq = max_len; p.S = prefix + max_len; p.W = bias ? W : 0; p.q_pos0 = prefix;
+  p.scale_log2 = scale * kLog2e;
+  p.cu = cu_seqlens; p.kv_cache = 1;
   return dispatch_prefill(p, d, dtype, (hipStream_t)stream);
 }
 

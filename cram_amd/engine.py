@@ -94,6 +94,12 @@ TAIL_SPLIT = os.environ.get("CRAM_TAIL_SPLIT", "1") != "0"
 # config 2 measured 75.75-75.94 q/s at 32k, 75.84 at 64k, 75.37 at 16k (r04, profiles/r04/ab_prefill_chunk/);
 # CRAM_PREFILL_CHUNK_ROWS overrides it (A/B)
 PREFILL_CHUNK_ROWS = int(os.environ.get("CRAM_PREFILL_CHUNK_ROWS", "32768"))
+# The prompts of one decode batch open with the same tokens (the chat template's system turn and the instruction line:
+# 37 of the ~906 tokens of a Llama-3 NQ prompt): their K/V are computed once, copied into every cache row, and the
+# packed prefill runs the suffixes only, attending over the cache (cram_attn_prefill_varlen_cached).
+# CRAM_PREFIX_SHARE=0 prefills whole prompts (A/B, tests).
+PREFIX_SHARE = os.environ.get("CRAM_PREFIX_SHARE", "1") != "0"
+PREFIX_SHARE_MIN_ROWS = 16
 
 
 def padded_rows(M: int, spec: Optional["ModelSpec"] = None) -> int:
@@ -507,6 +513,7 @@ class CrAMEngine:
             phases["steps"].record()
             phases["n_steps"] = n_steps
             phases["lens"] = list(sess.lens)
+            phases["prefix"] = int(getattr(sess, "prefix", 0))
         out = []
         gen = sess.generated().cpu().tolist()
         for row in gen:
@@ -733,6 +740,50 @@ class DecodeSession:
             (self.seen if rows is None else self.seen[rows]).scatter_(1, nxt[:, None], True)
         return nxt
 
+    def shared_prefix(self) -> int:
+        """Rows every prompt of the batch shares at its start, unbiased in every row (the credibility weights are 1
+        there, so those rows' attention is the same in every prompt), each prompt keeping >= 1 row of its own; 0 when
+        fewer than PREFIX_SHARE_MIN_ROWS."""
+        if not PREFIX_SHARE or self.B < 2:
+            return 0
+        n = min(self.lens) - 1
+        if n < PREFIX_SHARE_MIN_ROWS:
+            return 0
+        ids = torch.stack([p[:n] for p in self.prompts])
+        diff = (ids != ids[:1]).any(0)
+        p = int(diff.nonzero()[0, 0]) if bool(diff.any()) else n
+        Wp = min(p, self.cb.W)
+        if Wp > 0:
+            nz = (self.cb.bias[:, :Wp] != 0).any(0)
+            if bool(nz.any()):
+                p = int(nz.nonzero()[0, 0])
+        return p if p >= PREFIX_SHARE_MIN_ROWS else 0
+
+    def _prefill_prefix(self, p: int):
+        """The shared prefix once (rows 0..p-1 of prompt 0: causal, unbiased), its K/V of every layer into cache row
+        0, then copied to every other row."""
+        eng, sp = self.eng, self.eng.spec
+        h = eng.embed[self.prompts[0][:p]]
+        m = None
+        for l, lw in enumerate(eng.layers):
+            if m is None:
+                x = ops.rmsnorm(h, lw.ln1, sp.eps)
+            else:
+                h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
+            y = ops.linear(x, lw.wqkv, lw.bqkv)
+            ops.rope_split(y, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, p,
+                           self.k_cache[l][:1].transpose(1, 2), self.v_cache[l][:1].transpose(1, 2), 0, keep_k=True)
+            self.k_cache[l][1:, :, :p] = self.k_cache[l][:1, :, :p]
+            self.v_cache[l][1:, :, :p] = self.v_cache[l][:1, :, :p]
+            if l == sp.num_layers - 1:              # the last layer's K/V are all the prefix contributes
+                break
+            q = y[:, :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))[None]
+            k = y[:, sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))[None]
+            v = y[:, sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))[None]
+            a = eng.attention(q, k, v)
+            h, x2 = ops.rmsnorm(ops.linear(a.reshape(p, sp.q_size), lw.wo), lw.ln2, sp.eps, residual=h)
+            m = eng.mlp(x2, lw)
+
     def prefill(self, max_rows: int = PREFILL_CHUNK_ROWS):
         """All prompts in packed varlen passes of at most ``max_rows`` tokens each (GEMM M = the chunk's token
         count rounded to 256 rows; attention per sequence through cram_attn_prefill_varlen; K/V scattered into
@@ -741,32 +792,36 @@ class DecodeSession:
         the same blocks across chunks and calls (one 231k-row pass made it map fresh multi-GB segments, a ~1 s
         host stall per call)."""
         b0 = 0
+        self.prefix = p = self.shared_prefix()
         with gemm_tune.pinned():
+            if p:
+                self._prefill_prefix(p)
             while b0 < self.B:
                 b1, rows = b0, 0
-                while b1 < self.B and (b1 == b0 or rows + self.lens[b1] <= max_rows):
-                    rows += self.lens[b1]
+                while b1 < self.B and (b1 == b0 or rows + self.lens[b1] - p <= max_rows):
+                    rows += self.lens[b1] - p
                     b1 += 1
-                self._prefill_chunk(b0, b1)
+                self._prefill_chunk(b0, b1, p)
                 b0 = b1
         self.out[:, 0] = self.tokens
         self.t.fill_(1)
 
-    def _prefill_chunk(self, b0: int, b1: int):
+    def _prefill_chunk(self, b0: int, b1: int, p: int = 0):
+        """Prompts b0..b1-1 from row p on (p = the shared prefix already in the cache, or 0), packed."""
         eng, sp = self.eng, self.eng.spec
         dev = eng.device
-        lens = self.lens[b0:b1]
+        lens = [n - p for n in self.lens[b0:b1]]
         total = sum(lens)
         Mp = padded_rows(total, sp)
         offs = [0]
         for n in lens:
             offs.append(offs[-1] + n)
         cu = torch.tensor(offs, dtype=torch.int32).to(dev, non_blocking=True)
-        pos = torch.cat([torch.arange(n, dtype=torch.long) for n in lens]).to(dev, non_blocking=True)
+        pos = torch.cat([torch.arange(p, p + n, dtype=torch.long) for n in lens]).to(dev, non_blocking=True)
         bidx = torch.cat([torch.full((n,), b, dtype=torch.long) for b, n in enumerate(lens, b0)]).to(
             dev, non_blocking=True)
         h = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=dev)
-        h[:total] = eng.embed[torch.cat(self.prompts[b0:b1])]
+        h[:total] = eng.embed[torch.cat([t[p:] for t in self.prompts[b0:b1]])]
         if Mp > total:
             h[total:].zero_()
         bias = self.cb.bias[b0:b1]
@@ -777,16 +832,17 @@ class DecodeSession:
                 x = ops.rmsnorm(h, lw.ln1, sp.eps)
             else:
                 h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
-            # q and k roped in place (the varlen attention reads them there), roped k and v also written straight
-            # into the cache rows (sequence bidx, position pos) of this layer
+            # q roped in place, roped k and v written straight into the cache rows (sequence bidx, position pos) of
+            # this layer; k also kept in place when the packed attention reads it there (no shared prefix)
             kc, vc = self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2)
             if eng._fused_qkv_ok(x, lw):
                 y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1,
-                                  rows=total, kout=kc, vout=vc, row0=0, pos=pos, dst_b=bidx, keep_k=True, bias=lw.bqkv)
+                                  rows=total, kout=kc, vout=vc, row0=0, pos=pos, dst_b=bidx, keep_k=p == 0,
+                                  bias=lw.bqkv)
             else:
                 y = ops.linear(x, lw.wqkv, lw.bqkv)
                 ops.rope_split(y[:total], sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, 1, kc, vc,
-                               0, pos=pos, dst_b=bidx, keep_k=True)
+                               0, pos=pos, dst_b=bidx, keep_k=p == 0)
             yr = y[:total]
             q = yr[:, :sp.q_size].view(total, sp.num_heads, sp.head_dim)
             if l == sp.num_layers - 1:
@@ -804,9 +860,14 @@ class DecodeSession:
             a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
             if Mp > total:
                 a[total:].zero_()
-            ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=bias,
-                                    enable=self.cb.enable[l, b0:b1], W=self.cb.W,
-                                    out=a[:total].view(total, sp.num_heads, sp.head_dim))
+            if p:                                    # keys: the cached prefix, then the suffix's own rows
+                ops.attn_prefill_varlen_cached(q, kc[b0:b1], vc[b0:b1], cu, max(lens), p, scale=eng.scale, bias=bias,
+                                               enable=self.cb.enable[l, b0:b1], W=self.cb.W,
+                                               out=a[:total].view(total, sp.num_heads, sp.head_dim))
+            else:
+                ops.attn_prefill_varlen(q, k, v, cu, max(lens), scale=eng.scale, bias=bias,
+                                        enable=self.cb.enable[l, b0:b1], W=self.cb.W,
+                                        out=a[:total].view(total, sp.num_heads, sp.head_dim))
             h, x2 = eng.o_proj_norm(a, lw, h)
             h, m = eng.mlp_residual(x2, lw, h)
         hn = ops.rmsnorm(h, eng.norm, sp.eps) if m is None else ops.rmsnorm(m, eng.norm, sp.eps, residual=h)[1]

@@ -202,6 +202,40 @@ def attn_prefill_varlen(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_se
     return out
 
 
+def attn_prefill_varlen_cached(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, cu_seqlens: torch.Tensor,
+                               max_len: int, prefix: int, *, scale: float, bias: Optional[torch.Tensor] = None,
+                               enable: Optional[torch.Tensor] = None, W: int = 0,
+                               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Packed prompt suffixes over cached keys: q [total, Hq, d] (sequence b = tokens [cu[b], cu[b+1]), at positions
+    prefix + i), k/v [B, S, Hkv, d] views of the KV cache (token-major, any strides) whose rows 0 .. prefix + len_b - 1
+    hold the shared prefix and sequence b's own keys.  Returns out [total, Hq, d]."""
+    _check16("q", q, 3)
+    _check16("k", k, 4, q)
+    _check16("v", v, 4, q)
+    total, Hq, d = q.shape
+    B, S, Hkv, _ = k.shape
+    if v.shape != k.shape or k.shape[3] != d:
+        raise ValueError(f"shape mismatch q{tuple(q.shape)} k{tuple(k.shape)} v{tuple(v.shape)}")
+    if cu_seqlens.dtype != torch.int32 or not cu_seqlens.is_cuda or cu_seqlens.numel() != B + 1:
+        raise ValueError("cu_seqlens must be a device int32 [B+1] tensor (one entry per cache row + 1)")
+    if prefix < 0 or prefix + max_len > S:
+        raise ValueError(f"prefix {prefix} + max_len {max_len} exceeds the cache's {S} rows")
+    if out is None:
+        out = torch.empty((total, Hq, d), dtype=q.dtype, device=q.device)
+    bp, bsb, ep, esb, W = _bias_args(bias, enable, B, Hq, W)
+    flops, nbytes = prefill_work(1, Hq, Hkv, max_len, prefix + max_len, d, prefix)
+    ev = TIMER.record("cram_prefill_varlen", flops * B, nbytes * B, q.device) if TIMER.enabled else None
+    code = _lib.load().cram_attn_prefill_varlen_cached(
+        q.data_ptr(), q.stride(1), q.stride(0), k.data_ptr(), k.stride(0), k.stride(2), k.stride(1),
+        v.data_ptr(), v.stride(0), v.stride(2), v.stride(1), out.data_ptr(), out.stride(1), out.stride(0),
+        cu_seqlens.data_ptr(), B, int(max_len), int(prefix), Hq, Hkv, d, float(scale), bp, bsb, ep, esb, W, _dt(q),
+        _stream(q.device))
+    _lib.check(code, "cram_attn_prefill_varlen_cached")
+    if ev is not None:
+        ev.record(torch.cuda.current_stream(q.device))
+    return out
+
+
 def decode_workspace_bytes(B: int, Hq: int, d: int, num_splits: int) -> int:
     return int(_lib.load().cram_attn_decode_workspace_size(B, Hq, d, num_splits))
 

@@ -48,10 +48,10 @@ extern "C" {
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
 
-#define CRAM_ABI_VERSION 6        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
+#define CRAM_ABI_VERSION 7        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
                                      4: cram_get_knob(which, *value), decode projection GEMM;
                                      5: cram_gemm_residual, cram_gemm_rope, cram_gemm_splitk_residual;
-                                     6: cram_gemm_small */
+                                     6: cram_gemm_small; 7: cram_attn_prefill_varlen_cached */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -122,6 +122,21 @@ int cram_attn_prefill_varlen(const void* q, int64_t q_sh, int64_t q_st, const vo
                              const int32_t* cu_seqlens, int B, int max_len, int Hq, int Hkv, int d, float scale,
                              const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
                              int dtype, cram_stream_t stream);
+
+/*
+ * (ABI 7) Packed prefill of prompt SUFFIXES whose keys sit in a KV cache behind a shared prefix (the batched decode's
+ * prefill when every prompt starts with the same `prefix` tokens, computed once): sequence b's queries are tokens
+ * [cu_seqlens[b], cu_seqlens[b+1]) of q / o ([token][head][d]) at absolute positions prefix + i; its keys / values
+ * are rows 0 .. prefix + len_b - 1 of cache row b: k + b k_sb + j k_st + h k_sh (the prefix's rows, then its own,
+ * already written).  Causal from the row's position; bias row b indexes absolute key positions.  max_len >= every
+ * suffix length.  Same arithmetic as cram_attn_prefill_varlen over the whole prompts.
+ */
+int cram_attn_prefill_varlen_cached(const void* q, int64_t q_sh, int64_t q_st, const void* k, int64_t k_sb,
+                                    int64_t k_sh, int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh,
+                                    int64_t v_st, void* o, int64_t o_sh, int64_t o_st, const int32_t* cu_seqlens,
+                                    int B, int max_len, int prefix, int Hq, int Hkv, int d, float scale,
+                                    const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                                    int dtype, cram_stream_t stream);
 
 /*
  * Single-token decode attention (replaces the hooked SDPA call for q_len == 1;

@@ -70,6 +70,23 @@ def attn_prefill_varlen(q, k, v, cu_seqlens, max_len, *, scale, bias=None, enabl
     return res
 
 
+def attn_prefill_varlen_cached(q, k, v, cu_seqlens, max_len, prefix, *, scale, bias=None, enable=None, W=0,
+                               out=None):
+    cu = cu_seqlens.tolist()
+    res = torch.empty(q.shape, dtype=q.dtype)
+    for b in range(len(cu) - 1):
+        a, e = cu[b], cu[b + 1]
+        S = prefix + e - a
+        o = attn_prefill(q[a:e].transpose(0, 1)[None], k[b:b + 1, :S].transpose(1, 2), v[b:b + 1, :S].transpose(1, 2),
+                         scale=scale, q_pos0=prefix, bias=None if bias is None else bias[b:b + 1],
+                         enable=None if enable is None else enable[b:b + 1], W=W)
+        res[a:e] = o[0]
+    if out is not None:
+        out.copy_(res)
+        return out
+    return res
+
+
 def answer_logits(hidden, w_lm, ids, *, round_logits=False, out=None):
     r = (hidden.float() * w_lm[ids.long()].float()).sum(-1)
     if round_logits:
@@ -146,7 +163,7 @@ def gemm_splitk(x, w, splits, epilogue=0, bias=None, workspace=None, out=None, n
 def patched_ops():
     """Route cram_amd.ops through the CPU stand-ins for the duration of a CPU test."""
     from cram_amd import ops
-    names = ("attn_prefill", "attn_prefill_varlen", "attn_decode", "answer_logits", "decode_workspace_bytes",
+    names = ("attn_prefill", "attn_prefill_varlen", "attn_prefill_varlen_cached", "attn_decode", "answer_logits", "decode_workspace_bytes",
              "rmsnorm", "rope_inplace", "rope_split", "silu_mul", "gemm_splitk", "gemm_splitk_workspace_bytes")
     saved = {n: getattr(ops, n) for n in names}
     g = globals()

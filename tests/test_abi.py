@@ -30,7 +30,7 @@ def test_library_builds_loads_and_exports_every_symbol():
         assert hasattr(lib, n), n
     assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
     L = _lib.load()
-    assert L.cram_abi_version() == _lib.ABI_VERSION == 6
+    assert L.cram_abi_version() == _lib.ABI_VERSION == 7
     assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0

@@ -188,3 +188,29 @@ def test_config5_step_at_128_rows(l3w, monkeypatch):
     assert frac >= 0.5 and rows >= len(got) // 4
     dropin = _dropin_ids(eng, heads, prompts, ws, [0, 127], new)
     assert _check_dropin(got, dropin) >= 4
+
+
+def test_shared_prefix_prefill_at_llama3_widths(l3w, monkeypatch):
+    """The batch's common chat-template opening prefilled once, the suffixes over the cache
+    (cram_attn_prefill_varlen_cached), against whole-prompt prefill (CRAM_PREFIX_SHARE off): the prefix's K/V equal
+    the whole-prompt prefill's within bf16 GEMM-order noise, and the greedy ids agree up to near-ties."""
+    from cram_amd import engine as E
+    eng, tok, heads = l3w
+    prompts, ws = _encode(tok, 64)
+    new = 12
+    s = E.DecodeSession(eng, prompts, ws, heads, new)
+    s.prefill()
+    p = s.prefix
+    assert p >= E.PREFIX_SHARE_MIN_ROWS, p
+    monkeypatch.setattr(E, "PREFIX_SHARE", False)
+    s0 = E.DecodeSession(eng, prompts, ws, heads, new)
+    s0.prefill()
+    assert s0.prefix == 0
+    for c, c0 in ((s.k_cache, s0.k_cache), (s.v_cache, s0.v_cache)):
+        a, b = c[:, :, :, :p].float(), c0[:, :, :, :p].float()
+        assert (a - b).abs().max() <= 0.05 * b.abs().max() + 0.05, (a - b).abs().max()
+    whole = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
+    monkeypatch.setattr(E, "PREFIX_SHARE", True)
+    shared = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
+    rows, frac = _compare(eng, heads, prompts, ws, shared, whole, "shared-prefix vs whole-prompt prefill")
+    assert frac >= 0.5 and rows >= len(shared) // 4

@@ -16,6 +16,7 @@ import pytest
 import torch
 
 from cram_amd import spans as S
+import cram_amd.engine as engine_mod
 from cram_amd.engine import CrAMEngine, DecodeSession
 from cram_amd import sweep
 from oracle import hook_ref
@@ -209,6 +210,9 @@ def test_engine_batched_generate_matches_single(tiny, nq):
         chunked, whole = DecodeSession(eng, prompts, ws, heads, 5), DecodeSession(eng, prompts, ws, heads, 5)
         chunked.prefill(max_rows=340)
         whole.prefill()
+    # the batch's prompts share their chat-template opening: it is prefilled once and the suffixes attend over the
+    # cache (cram_attn_prefill_varlen_cached); the single-prompt runs prefill whole prompts
+    assert whole.prefix >= engine_mod.PREFIX_SHARE_MIN_ROWS, whole.prefix
     assert both == one
     # the decode step's projections on the split-K GEMM (cram_gemm_splitk; CRAM_DECODE_GEMM=all routes every
     # projection of the tiny shapes through it) == F.linear

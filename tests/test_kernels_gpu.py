@@ -310,6 +310,42 @@ def test_prefill_varlen_matches_oracle(gpu_device, prefill_variant, lens, Hq, Hk
     _check(out, ref)
 
 
+@pytest.mark.parametrize("prefix,lens,Hq,Hkv", [(37, [300, 17, 129, 1], 32, 8), (16, [900, 77], 8, 2),
+                                                (64, [5, 6, 7], 7, 1)])
+def test_prefill_varlen_cached_matches_oracle(gpu_device, prefill_variant, prefix, lens, Hq, Hkv):
+    """Packed prompt suffixes over a KV cache holding a shared prefix (cram_attn_prefill_varlen_cached, the batched
+    decode's prefill with the chat-template opening computed once) == each sequence's suffix rows through the oracle
+    over [prefix | suffix] keys, with the bias on absolute key positions."""
+    from cram_amd import ops
+    gen = torch.Generator().manual_seed(prefix + sum(lens))
+    d, B = 128, len(lens)
+    S_max = prefix + max(lens) + 8
+    bf = torch.bfloat16
+    kc = torch.zeros((B, Hkv, S_max, d), dtype=bf)
+    vc = torch.zeros_like(kc)
+    kc[:, :, :prefix] = torch.randn(Hkv, prefix, d, generator=gen).to(bf)
+    vc[:, :, :prefix] = torch.randn(Hkv, prefix, d, generator=gen).to(bf)
+    W = prefix + max(lens)
+    lw, bias, enable, heads = _bias_inputs(B, Hq, W, W, gen)
+    qs, refs, cu = [], [], [0]
+    for b, n in enumerate(lens):
+        kc[b, :, prefix:prefix + n] = torch.randn(Hkv, n, d, generator=gen).to(bf)
+        vc[b, :, prefix:prefix + n] = torch.randn(Hkv, n, d, generator=gen).to(bf)
+        q = torch.randn(Hq, n, d, generator=gen).to(bf)
+        S = prefix + n
+        refs.append(hook_ref.biased_attention_ref(q[None], kc[b:b + 1, :, :S], vc[b:b + 1, :, :S],
+                                                  lw[b:b + 1, :min(W, S)], [heads[b]], d ** -0.5)[0])
+        qs.append(q.transpose(0, 1))
+        cu.append(cu[-1] + n)
+    dev = gpu_device
+    kd, vd = kc.to(dev), vc.to(dev)
+    out = ops.attn_prefill_varlen_cached(torch.cat(qs).contiguous().to(dev), kd.transpose(1, 2), vd.transpose(1, 2),
+                                         torch.tensor(cu, dtype=torch.int32, device=dev), max(lens), prefix,
+                                         scale=d ** -0.5, bias=bias.to(dev), enable=enable.to(dev), W=W)
+    torch.cuda.synchronize()
+    _check(out, torch.cat(refs, 0))
+
+
 def _rows_ref(q, k, v, bias, enable, W, scale, b, h, rows, G):
     """float64 reference for a few query rows of one (batch, head): causal over keys <= row (q_pos0 = 0),
     bias[b, j] added for j < W when the head is enabled (the hook's semantics, re_weighting.py:57-59)."""
