@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes for the sweep's dominant GEMM launch (gemm_w4_kernel, gate/up + SiLU-mul at M = 29,184): separate --pmc
 # runs, kernel-trace only, the same counter sets as tools/pmc_attn.sh (MI355X_MICROARCH.md HBM / rocprofv3).
+# MODE=lt KREGEX=Cijk: hipBLASLt's kernel for the same product (comparison); MODE=store: the plain-store epilogue.
 set -e
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -8,8 +9,8 @@ OUT=${OUT:-$R/gpurun_out/gemm_pmc}
 mkdir -p $OUT
 run() {
   name=$1; shift
-  timeout -k 10 180 rocprofv3 --kernel-include-regex 'gemm_w4_kernel' --pmc "$@" --kernel-trace --output-format csv \
-    -d $OUT/$name -o $name -- python3 tools/gemm_pmc.py 29184 4 > $OUT/$name.log 2>&1
+  timeout -k 10 180 rocprofv3 --kernel-include-regex "${KREGEX:-gemm_w4_kernel}" --pmc "$@" --kernel-trace \
+    --output-format csv -d $OUT/$name -o $name -- python3 tools/gemm_pmc.py 29184 4 ${MODE:-silu} > $OUT/$name.log 2>&1
 }
 run p1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES
 run p2 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE

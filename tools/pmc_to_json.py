@@ -29,8 +29,9 @@ sys.path.insert(0, REPO)
 from cram_amd.build import gemm_source_hash, kernel_source_hash  # noqa: E402
 from cram_amd.ops import prefill_work  # noqa: E402
 
-GEMM = "--gemm" in sys.argv
-ARGS = [a for a in sys.argv[1:] if a != "--gemm"]
+GEMM = "--gemm" in sys.argv or "--lt" in sys.argv
+LT = "--lt" in sys.argv          # hipBLASLt's kernel for the same [gate; up] product (MODE=lt tools/pmc_gemm.sh)
+ARGS = [a for a in sys.argv[1:] if a not in ("--gemm", "--lt")]
 B, T, Hq, Hkv, d = 33, 962, 32, 8, 128          # tools/prof_attn.py's default: the IE sweep's attention launch
 GM, GN, GK = 29184, 28672, 4096                  # tools/gemm_pmc.py: gate/up (+ SiLU-mul, output N / 2 wide)
 SIMDS = 1024                                     # 256 CUs x 4 SIMDs
@@ -64,7 +65,7 @@ def main():
     dst = ARGS[1] if len(ARGS) > 1 else os.path.join(REPO, "profiles", "gemm_pmc.json" if GEMM else "attn_pmc.json")
     c, kernels = load(src)
     if GEMM:
-        flops, alg_bytes = 2.0 * GM * GN * GK, 2.0 * (GM * GK + GN * GK + GM * GN // 2)
+        flops, alg_bytes = 2.0 * GM * GN * GK, 2.0 * (GM * GK + GN * GK + GM * (GN if LT else GN // 2))
     else:
         flops, alg_bytes = prefill_work(B, Hq, Hkv, T, T, d, 0)
     read_b = mean(c["FETCH_SIZE"]) * 1024 * 2
@@ -80,7 +81,7 @@ def main():
     n_mfma = mean(c["SQ_INSTS_MFMA"])
     out = {
         "kernel": " / ".join(sorted(kernels)),
-        "shape": ({"M": GM, "N": GN, "K": GK, "epilogue": "SiLU-mul"} if GEMM else
+        "shape": ({"M": GM, "N": GN, "K": GK, "epilogue": "store (hipBLASLt F.linear)" if LT else "SiLU-mul"} if GEMM else
                   {"B": B, "T": T, "Hq": Hq, "Hkv": Hkv, "d": d}),
         "dispatches": len(c["FETCH_SIZE"]),
         "fetch_size_kib": mean(c["FETCH_SIZE"]), "write_size_kib": mean(c["WRITE_SIZE"]),
@@ -98,7 +99,7 @@ def main():
         "wait_any_frac": round(mean(c["SQ_WAIT_ANY"]) / mean(c["SQ_WAVE_CYCLES"]), 4),
         "lds_bank_conflict_per_lds_inst": round(mean(c["SQ_LDS_BANK_CONFLICT"]) / mean(c["SQ_INSTS_LDS"]), 4),
         "source": os.path.relpath(os.path.abspath(src), REPO),
-        "kernel_source_hash": gemm_source_hash() if GEMM else kernel_source_hash(),
+        "kernel_source_hash": None if LT else (gemm_source_hash() if GEMM else kernel_source_hash()),
         "note": (f"rocprofv3 --pmc in separate passes (tools/{'pmc_gemm' if GEMM else 'pmc_attn'}.sh). traffic: "
                  "FETCH_SIZE x2 (gfx950 16 B/lane "
                  "read undercount) + WRITE_SIZE, KiB -> B; hbm_gbs / tflops: over the dispatches' own wall time; "
