@@ -341,6 +341,16 @@ class CrAMEngine:
             lw.wgu_il_key = key
         return lw.wgu_il
 
+    def _gate_up_tail(self, lw: LayerW, c0: int) -> torch.Tensor:
+        """[gate[c0:]; up[c0:]] of lw.wgu (the split-K SiLU-mul layout) for the decode step's column tail, rebuilt
+        whenever the checkpoint weight changes."""
+        w, F = lw.wgu, self.spec.intermediate
+        key = (w.data_ptr(), w._version, c0)
+        if getattr(lw, "wgu_tail_key", None) != key:
+            lw.wgu_tail = torch.cat([w[c0:F], w[F + c0:]]).contiguous()
+            lw.wgu_tail_key = key
+        return lw.wgu_tail
+
     def qkv(self, x: torch.Tensor, lw: LayerW, cos, sin, pos: Optional[torch.Tensor] = None):
         """x [B, T, D] -> roped q [B, T, Hq, d], k / v [B, T, Hkv, d]: strided views of one fused buffer."""
         sp = self.spec
@@ -677,9 +687,32 @@ class DecodeSession:
                        and (2 * sp.intermediate, sp.hidden) == (28672, 4096)     # the measured shape only
                        and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))
                        and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
-        if self.mlp_w4:
+        # gate/up where the 4-wave kernel's 256 x 256 tiles spill just past one wave of the CUs (Qwen2-7B at 512 rows:
+        # N 37,888 = 148 column tiles x 2 row tiles = 296 tiles = 1.16 waves, so the kernel took two tile times and
+        # lost to hipBLASLt, 167.8 vs 153 us): the columns of one whole wave on it (+ SiLU-mul), the rest through the
+        # split-K GEMM with K cut until the tail fills the CUs (+ SiLU-mul in its combine, on [gate; up] rows of the
+        # tail).  CRAM_DECODE_MLP_TAIL=0 keeps the library (A/B).
+        self.mlp_tail = None
+        if (not self.mlp_w4 and not self.splits_gemm["gu"] and self.B >= DECODE_MLP_W4_MIN_ROWS
+                and eng.device.type == "cuda" and os.environ.get("CRAM_DECODE_MLP_TAIL", "1") != "0"
+                and os.environ.get("CRAM_DECODE_GEMM", "1") != "0"
+                and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))):
+            ntm, ntn, cus = -(-self.B // 256), 2 * F // 256, eng.num_cus
+            if cus < ntm * ntn < cus * 3 // 2 and cus % ntm == 0:
+                c0 = (cus // ntm) * 128                  # output columns of the whole wave (a tile = 128 outputs)
+                tail_tiles = ntm * -(-2 * (F - c0) // 256)
+                kt = D // 64
+                s_best = 0
+                for sv in range(1, kt + 1):
+                    if kt % sv == 0 and tail_tiles * sv <= cus and kt // sv >= 4:
+                        s_best = sv
+                if s_best and F - c0 >= 64:
+                    self.mlp_tail = (c0, s_best)
+        if self.mlp_w4 or self.mlp_tail:
             for lw in eng.layers:
                 eng._gate_up_interleaved(lw)
+                if self.mlp_tail:
+                    eng._gate_up_tail(lw, self.mlp_tail[0])
         # lm_head on the 4-wave kernel (vocab % 256 == 0): 225 vs 290 us at 129 rows, 418 vs 457 at 512 (Llama-3)
         self.lm_w4 = (eng.device.type == "cuda" and eng.dtype in (torch.bfloat16, torch.float16)
                       and eng.lm_head.shape[0] % 256 == 0
@@ -692,8 +725,10 @@ class DecodeSession:
         self.small = {k: v for k, v in self.small.items() if v}
         for k in self.small:
             self.splits_gemm[k] = 0
+        tail = [] if not self.mlp_tail else [(2 * (F - self.mlp_tail[0]), self.mlp_tail[1])]
         need = max([ops.gemm_splitk_workspace_bytes(self.B, shapes[k], v) for k, v in
-                    list(self.splits_gemm.items()) + list(self.small.items()) if v] or [0])
+                    list(self.splits_gemm.items()) + list(self.small.items()) if v]
+                   + [ops.gemm_splitk_workspace_bytes(self.B, n, v) for n, v in tail] or [0])
         self.gemm_ws = torch.empty(need, dtype=torch.uint8, device=dev) if need else None
 
     def _proj(self, x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], key: str) -> torch.Tensor:
@@ -706,7 +741,16 @@ class DecodeSession:
 
     def _mlp(self, x: torch.Tensor, lw: LayerW) -> torch.Tensor:
         s = self.splits_gemm["gu"]
-        if self.mlp_w4:
+        if self.mlp_tail:
+            c0, st = self.mlp_tail
+            F = self.eng.spec.intermediate
+            x2 = x.reshape(-1, x.shape[-1])
+            act = torch.empty((x2.shape[0], F), dtype=x.dtype, device=x.device)
+            ops.gemm(x2, self.eng._gate_up_interleaved(lw)[:2 * c0], ops.GEMM_SILU_MUL, out=act[:, :c0])
+            ops.gemm_splitk(x2, self.eng._gate_up_tail(lw, c0), st, ops.GEMM_SILU_MUL_CAT, workspace=self.gemm_ws,
+                            out=act[:, c0:])
+            act = act.view(*x.shape[:-1], F)
+        elif self.mlp_w4:
             act = ops.gemm(x, self.eng._gate_up_interleaved(lw), ops.GEMM_SILU_MUL)
         elif s:
             act = ops.gemm_splitk(x, lw.wgu, s, ops.GEMM_SILU_MUL_CAT, workspace=self.gemm_ws)

@@ -20,8 +20,11 @@ import os
 
 GUARD_F = 4.0
 GUARD_A = {"ie_mean": 0.01, "ie_max": 0.05, "logprob_max": 0.01}
-AGG_F = {"ie_mean": 1.5, "ie_max": 1.5, "logprob_max": 1.5}
-AGG_F_CPU = {"ie_mean": 2.5, "ie_max": 2.5}
+# worst aggregate measured on the round-5 GPU suite + 25 % (ie_mean 1.141 llama2, ie_max 0.971 qwen2 over 8
+# questions, logprob_max 1.093 qwen2) and on the CPU stand-ins (ie_mean 1.957, ie_max 1.630):
+# profiles/r05/parity_ratios.json
+AGG_F = {"ie_mean": 1.43, "ie_max": 1.21, "logprob_max": 1.37}
+AGG_F_CPU = {"ie_mean": 2.45, "ie_max": 2.04}
 
 
 def record(family: str, ours: float, ref: float, **extra) -> None:

@@ -139,3 +139,38 @@ def test_config4_answer_logprobs_match_reference_hook(qwen7):
     finally:
         del m16, m32
         torch.cuda.empty_cache()
+
+
+def test_config4_gate_up_column_tail_at_512_rows(qwen7):
+    """Config 4's decode step at 512 rows: gate/up (N 37,888 = 296 tiles of 256 x 256, 1.16 waves) on the 4-wave
+    kernel for one whole wave of columns + the split-K column tail (DecodeSession.mlp_tail) == the float32 MLP
+    activation within bf16 rounding, and no further from it than the library path (hipBLASLt + cram_silu_mul)."""
+    from cram_amd import ops
+    from cram_amd.engine import DecodeSession
+    obj, _, _ = qwen7
+    eng = obj.engine
+    sp = eng.spec
+    g = torch.Generator(device=eng.device).manual_seed(5)
+    prompts = [torch.randint(0, 1000, (40,), device=eng.device, generator=g) for _ in range(512)]
+    ws = [torch.ones((1, 40), dtype=torch.float16) for _ in range(512)]
+    s = DecodeSession(eng, prompts, ws, {}, 4)
+    if eng.num_cus != 256:
+        pytest.skip("the column split is sized for 256 CUs")
+    assert s.mlp_tail == (16384, 4), s.mlp_tail
+    lw = eng.layers[0]
+    x = (torch.randn((512, 1, sp.hidden), device=eng.device, generator=g) * 0.5).to(eng.dtype)
+    F = sp.intermediate
+    got = ops.gemm(x.view(512, -1), eng._gate_up_interleaved(lw)[:2 * 16384], ops.GEMM_SILU_MUL)
+    full = torch.empty((512, F), dtype=eng.dtype, device=eng.device)
+    full[:, :16384] = got
+    ops.gemm_splitk(x.view(512, -1), eng._gate_up_tail(lw, 16384), 4, ops.GEMM_SILU_MUL_CAT, out=full[:, 16384:])
+    lib = ops.silu_mul(ops.linear(x.view(512, -1), lw.wgu), F)
+    gu = x.view(512, -1).float() @ lw.wgu.float().t()
+    ref = torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]
+    e_new, e_lib = (full.float() - ref).abs(), (lib.float() - ref).abs()
+    scale = ref.abs().max()
+    assert e_new.max() <= 0.02 * scale, (float(e_new.max()), float(scale))
+    assert e_new.mean() <= 1.25 * e_lib.mean() + 1e-6, (float(e_new.mean()), float(e_lib.mean()))
+    # and the session's own step MLP runs the same split (down_proj on its split-K) without error
+    y = s._mlp(x, lw)
+    assert y.shape == (512, 1, sp.hidden) and torch.isfinite(y.float()).all()
