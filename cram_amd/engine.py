@@ -149,7 +149,7 @@ def configure_blas(lib: str = "hipblas") -> None:
 
 
 class LayerW:
-    __slots__ = ("ln1", "wqkv", "bqkv", "wo", "ln2", "wgu", "wd", "wgu_il", "wgu_il_key")
+    __slots__ = ("ln1", "wqkv", "bqkv", "wo", "ln2", "wgu", "wd", "wgu_il", "wgu_il_key", "wgu_tail", "wgu_tail_key")
 
 
 class CrAMEngine:
