@@ -24,11 +24,11 @@ def asm(tmp_path_factory):
 
 
 def test_every_register_owning_instantiation_is_audited(asm):
-    """The audited list comes from the assembly: every epilogue (store, SiLU-mul, residual, RoPE) of gemm_w4_kernel in
-    both element types, and prefill_x32_kernel."""
+    """The audited list comes from the assembly: every epilogue (store, SiLU-mul, split-K partial, residual, RoPE) of
+    gemm_w4_kernel in both element types, and prefill_x32_kernel."""
     names = build.asm_kernels(asm)
     w4 = [n for n in names if "gemm_w4_kernel" in n]
-    for epi in ("Li0E", "Li1E", "Li101E", "Li102E"):
+    for epi in ("Li0E", "Li1E", "Li100E", "Li101E", "Li102E"):
         for dt in ("DF16b", "DF16_"):
             assert any(dt + epi in n for n in w4), (dt, epi, w4)
     assert any("prefill_x32_kernel" in n for n in names)
