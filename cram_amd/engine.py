@@ -94,6 +94,9 @@ TAIL_SPLIT = os.environ.get("CRAM_TAIL_SPLIT", "1") != "0"
 # config 2 measured 75.75-75.94 q/s at 32k, 75.84 at 64k, 75.37 at 16k (r04, profiles/r04/ab_prefill_chunk/);
 # CRAM_PREFILL_CHUNK_ROWS overrides it (A/B)
 PREFILL_CHUNK_ROWS = int(os.environ.get("CRAM_PREFILL_CHUNK_ROWS", "32768"))
+# the sweep's last suffix layer projects q for the answer rows only (layer_rows, out_rows + prefix);
+# CRAM_LAST_Q_ROWS=0 projects every row's q as the other layers do (A/B)
+LAST_Q_ROWS_ONLY = os.environ.get("CRAM_LAST_Q_ROWS", "1") != "0"
 # The prompts of one decode batch open with the same tokens (the chat template's system turn and the instruction line:
 # 37 of the ~906 tokens of a Llama-3 NQ prompt): their K/V are computed once, copied into every cache row, and the
 # packed prefill runs the suffixes only, attending over the cache (cram_attn_prefill_varlen_cached).
@@ -424,6 +427,23 @@ class CrAMEngine:
             k[:, :p0] = k0
             v[:, :p0] = v0
             # q roped in place; the suffix's roped k and its v land behind the prefix (no copy pass)
+            if fused and out_rows is not None and LAST_Q_ROWS_ONLY:
+                # the last layer reads q of the answer rows only: K / V of every row (the k | v rows of the fused
+                # weight), q of the last out_rows rows of every sequence (a 1/3-size GEMM over 2/3 of the columns)
+                n = out_rows
+                qs = sp.q_size
+                ops.gemm_rope(x, lw.wqkv[qs:], 0, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M, kout=k, vout=v,
+                              row0=p0, pos0=p0, bias=None if lw.bqkv is None else lw.bqkv[qs:])
+                xa = x[:M].view(B, T, -1)[:, -n:].reshape(B * n, -1)
+                yq = ops.gemm_rope(xa, lw.wqkv[:qs], sp.num_heads, 0, sp.head_dim, cos, sin, n,
+                                   pos0=p0 + T - n, bias=None if lw.bqkv is None else lw.bqkv[:qs])
+                q = yq.view(B, n, sp.num_heads, sp.head_dim)
+                a = torch.empty((B * n, sp.q_size), dtype=self.dtype, device=self.device)
+                ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale,
+                                 bias=bias, enable=enable, W=W, out=a.view(B, n, sp.num_heads, sp.head_dim))
+                hres = hbuf[:M].view(B, T, -1)[:, -n:].reshape(B * n, -1)
+                h2, x2 = self.o_proj_norm(a, lw, hres)
+                return self.mlp_residual(x2, lw, h2)
             if fused:
                 # the suffix rows' positions are p0 + t: no position loads
                 y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, rows=M,

@@ -231,6 +231,7 @@ int cram_gemm(const void* y, int64_t ldy, const void* x, int64_t ldx, void* out,
  * Rows in [rows, M) are GEMM padding: out rows written (q), nothing else.  bf16 / fp16, d = 128, K % 64 == 0,
  * K >= 128 (the 4-wave kernel), ldo % 8 == 0; pos / dst_b int64 device arrays of >= rows entries.  bias [N]
  * (16-byte aligned; Qwen2's q / k / v) or NULL: the projection is rnd(acc + bias), F.linear's rounding, before RoPE.
+ * Part of the fused weight: hq = 0 (y = the k | v rows: K / V only) or hkv = 0 (y = the q rows; no kout).
  */
 int cram_gemm_rope(const void* y, int64_t ldy, const void* x, int64_t ldx, const void* bias, void* out, int64_t ldo,
                    int M, int K, int rows, int T, int hq, int hkv, int d, const void* cos_t, const void* sin_t,

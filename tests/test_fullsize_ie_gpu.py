@@ -291,3 +291,28 @@ def test_sweep_outpaces_reference_algorithm_on_same_gpu(setup):
           f"({dt / (len(units) + 1) * 1e3:.1f} ms per hooked forward); head-batched sweep {ours:.1f} units/s "
           f"-> {ours / ref:.2f}x")
     assert ours > ref
+
+
+def test_last_layer_projects_q_of_the_answer_rows_only(setup):
+    """The last suffix layer of every variant batch projects K / V for every row and q for the answer rows only
+    (engine.layer_rows, LAST_Q_ROWS_ONLY): the 4-wave GEMM is row- and column-independent, so the variants' final
+    hidden states equal those of the full q/k/v projection bit for bit."""
+    from cram_amd import engine as E
+    from cram_amd import sweep
+    from cram_amd.bias import CredibilityBias
+
+    eng, ids, w16, ans = setup
+    sp = eng.spec
+    n = ans.numel()
+    cb = CredibilityBias.build([w16.view(1, -1)], {}, sp.num_layers, sp.num_heads, eng.device, eng.dtype)
+    p0 = sweep.first_biased_row(cb.bias, cb.W)
+    _, qc = sweep.baseline(eng, ids, n, p0=p0)
+    prev = E.LAST_Q_ROWS_ONLY
+    try:
+        outs = []
+        for flag in (True, False):
+            E.LAST_Q_ROWS_ONLY = flag
+            outs.append(sweep.layer_variants(eng, qc, 29, cb.bias, cb.W, n, p0=p0))
+    finally:
+        E.LAST_Q_ROWS_ONLY = prev
+    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max()
