@@ -41,9 +41,9 @@ from . import gemm_tune, ops
 from .bias import CredibilityBias
 from .engine import CrAMEngine, padded_rows
 
-# Opt-in (CRAM_SWEEP_ROW_EXACT=1): drop the un-perturbed variant where the arithmetic is row-exact.  +2.1 % heads/s,
-# but measured its IE grids trail the default's at the path's k = 894 (4,069 vs 4,127 truth-overlap
-# over 5 full grids) and it fails the frozen grid bar on the test question, so the default keeps the variant.
+# Opt-in (CRAM_SWEEP_ROW_EXACT=1): drop the un-perturbed variant where the arithmetic is row-exact.  +2.1 % heads/s;
+# over 13 full grids its IE error and k = 894 overlap equal the default's, but it fails the frozen
+# grid bar on that test's question (a ~1-sigma bar), so the default keeps the variant.
 ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "0") == "1"
 
 
