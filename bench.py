@@ -170,6 +170,9 @@ def main():
                     help="decode scores: ideal [0.1,1,1,1,1] or the NQ GPT truthful scores (RAG_test.py:89-105)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-prefix-skip", action="store_true", help="recompute rows before the first biased key (A/B)")
+    ap.add_argument("--position-sweep", action="store_true",
+                    help="config 3 as casual_tracing_per_head_with_position (find_best_heads.py:61-110): each question "
+                         "swept with the fake passage at positions 0..4 among the retrieved ones (5 x L x H units)")
     ap.add_argument("--cpu-units", type=int, default=64,
                     help="IE units of the CPU baseline sample (>= 1; BASELINE.md: 1 question x 2 layers x 32 heads)")
     ap.add_argument("--cpu-decode-questions", type=int, default=2,
@@ -241,13 +244,19 @@ def main():
         mean_c = sum(clen) / len(clen)
         pool = sorted(range(len(data)), key=lambda i: (abs(clen[i] - mean_c), i))
         work = []
+        from cram_amd import heads as Hd
+        positions = range(5) if args.position_sweep else (None,)
         for s in range(n_w + n_t):
             qi = pool[s % len(pool)]
             rec = data[qi]
-            _, enc, w, _ = spans.encode(tok, name, rec["question"], rec["ori_fake"] + rec["reranked_dense_ctxs"],
-                                        [0, 1, 1, 1, 1], rec["wrong_answer"])
             ans = tok([rec["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
-            work.append((qi, enc["input_ids"][0].to(dev), w[0], ans.to(dev)))
+            for pos in positions:
+                # the plain sweep's contexts (find_best_heads.py:41-48) or the fake passage at `pos` (:83-99)
+                ctx, sc = (Hd.position_contexts(rec, pos) if pos is not None
+                           else (rec["ori_fake"] + rec["reranked_dense_ctxs"], [0, 1, 1, 1, 1]))
+                _, enc, w, _ = spans.encode(tok, name, rec["question"], ctx, sc, rec["wrong_answer"])
+                work.append((qi, enc["input_ids"][0].to(dev), w[0], ans.to(dev)))
+        n_w, n_t = n_w * len(positions), n_t * len(positions)        # work items: (question, position)
         torch.cuda.synchronize()
         mine = []
 
@@ -278,11 +287,15 @@ def main():
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t_start
         ops.TIMER.enabled = False
-        flops = 0.0
+        flops = flops_ex = 0.0
+        base_variant = not sweep.row_exact(eng)
         for T, n_ans, w, layers in mine:
             p0 = int((w.view(-1) != 1).nonzero()[0, 0]) if bool((w != 1).any()) else T
             p0 = 0 if args.no_prefix_skip else p0
-            flops += sweep.sweep_flops(spec, T, n_ans, p0, layers, base_variant=not sweep.row_exact(eng))
+            # algorithmic (SURVEY §8(d) with the prefix skip: 32 variants, answer-row q in the last layer) and what
+            # the sweep executes (+ the un-perturbed variant of the default mode, the GEMMs' pad rows)
+            flops += sweep.sweep_flops(spec, T, n_ans, p0, layers)
+            flops_ex += sweep.sweep_flops_executed(spec, T, n_ans, p0, layers, base_variant=base_variant)
         ksum = ops.TIMER.summary()
         kt = ksum.get("cram_prefill", None)
         # the projections: cram_gemm (gemm_w4_kernel, every epilogue), its split-K tail, and F.linear calls left
@@ -298,13 +311,14 @@ def main():
         if kc is not None:
             kc["avg_ms"] = kc["total_ms"] / kc["launches"]
         el = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        fl = torch.tensor([flops], device=dev, dtype=torch.float64)
+        fl = torch.tensor([flops, flops_ex], device=dev, dtype=torch.float64)
         if world > 1:
             el, fl = cdist.all_reduce_host(el, "max"), cdist.all_reduce_host(fl, "sum")
-        elapsed, flops_all = float(el.item()), float(fl.item())
+        elapsed, flops_all, flops_ex_all = float(el.item()), float(fl[0].item()), float(fl[1].item())
         units = n_t * L * H
         assert tuple(full.shape) == (n_t, L, H) and torch.isfinite(full).all(), "non-finite or missing IE"
-        ie = {"value": units / elapsed, "elapsed": elapsed, "flops": flops_all, "kt": kt, "kg": kg, "kc": kc,
+        ie = {"value": units / elapsed, "elapsed": elapsed, "flops": flops_all, "flops_executed": flops_ex_all,
+              "base_variant": base_variant, "kt": kt, "kg": kg, "kc": kc,
               "mean_T": sum(x[1].numel() for x in work) / len(work), "work": work}
         log(f"[rank {rank}] IE sweep: {units} units in {elapsed:.2f}s -> {ie['value']:.1f} heads/s")
 
@@ -419,13 +433,15 @@ def main():
             f"decode attention {decode.get('attention_roofline', {}).get('achieved', 0):.0f} GB/s")
         del dev_prompts
 
-    # ------------------------------------------------------------------ CPU baselines (rank 0, N = 1)
+    # ------------------------------------------------------------------ CPU baselines (rank 0, any N)
     # the reference's own algorithm on the host cores (oracle/cpu_baseline.py): IE units (config 3) and the hooked
-    # greedy decode of one question (configs 2-5), sampled and extrapolated, after the timed regions
+    # greedy decode of one question (configs 2-5), sampled and extrapolated, after the timed regions.  At N > 1 the
+    # north star wants the CPU hook path next to the GPU numbers in the same run: rank 0 times it after every rank
+    # has left its timed regions; the other ranks wait at the final barrier (process-group timeout: cdist.init)
     cpu = cpu_dec = None
     want_ie = ie is not None
     want_dec = decode is not None and args.cpu_decode_steps > 0
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and (want_ie or want_dec):
+    if rank == 0 and not args.no_cpu_baseline and (want_ie or want_dec):
         from oracle import cpu_baseline
         t0 = time.time()
         cpu_model = cpu_baseline.hf_model_from_engine(eng)
@@ -565,9 +581,14 @@ def main():
                 "value": round(ie["value"], 3), "unit": "heads/s",
                 "ms_per_step": round(ie["elapsed"] * 1e3 / args.steps, 2), "scaling": "weak",
                 "data": f"synthetic: random-init {name} weights; rebuilt NQ-1000 prompts via offline BPE tokenizer",
-                "config": {"workload": f"{name} Find_Best_Heads IE sweep, {L} layers x {H} heads per question, "
-                                       "scores [0,1,1,1,1], 1 NQ question per GPU per step (config 3; decode = config 2)",
+                "config": {"workload": (f"{name} Find_Best_Heads IE sweep, {L} layers x {H} heads per question, "
+                                        "scores [0,1,1,1,1], 1 NQ question per GPU per step (config 3; decode = config 2)")
+                                       if not args.position_sweep else
+                                       (f"{name} casual_tracing_per_head_with_position (find_best_heads.py:61-110): "
+                                        f"{L} layers x {H} heads x fake passage at positions 0..4 per question, "
+                                        "1 NQ question per GPU per step"),
                            "questions_per_step": world,
+                           "units_per_question": L * H * (5 if args.position_sweep else 1),
                            "question_order": "nearest the mean NQ prompt length first; steps x N questions dealt to "
                                              "ranks by cram_amd.dist.plan (LPT on token counts)",
                            "mean_prompt_tokens": round(ie["mean_T"], 1),
@@ -577,7 +598,16 @@ def main():
                 "dominant_kernel": dom,
                 "step_roofline": {"bound": "mfma", "achieved": round(step_tf, 2), "peak": PEAK_BF16_TFLOPS * world,
                                   "unit": "TFLOP/s", "frac": round(step_tf / (PEAK_BF16_TFLOPS * world), 4),
-                                  "flops_per_question": ie["flops"] / max(1, world * args.steps)},
+                                  "flops_per_question": ie["flops"] / max(1, world * args.steps),
+                                  "flops_definition": "algorithmic, SURVEY §8(d) with the prefix skip: baseline "
+                                                      "forward + per layer the biased attention and 32 variants "
+                                                      "through the layers above, the last layer's q / attention / "
+                                                      "MLP on the answer rows only (sweep.sweep_flops)",
+                                  "executed_flops_per_question": ie["flops_executed"] / max(1, world * args.steps),
+                                  "executed_note": ("+ the un-perturbed 33rd variant per batch, " if ie["base_variant"]
+                                                    else "") + "+ the GEMMs' pad rows, the baseline's last-layer q "
+                                                               "over every row (sweep.sweep_flops_executed); not "
+                                                               "credited to frac"},
                 "cpu_baseline": cpu, "decode": decode})
             if cpu:
                 result["speedup_vs_cpu"] = round(ie["value"] / cpu["value"], 1)
@@ -673,6 +703,21 @@ def run_config1(args):
                          f"dense-mask hook on every layer (GPT-2 adapter), bf16 CPU, {cs:.1f}s"}
         log(f"[config 1] CPU hook path: {cpu['value']:.3f} questions/s on {cpu['cores']} cores")
     T_mean = sum(ids.shape[1] for ids, _ in prompts) / len(prompts)
+    # HBM roofline of the batch-1 decode (what bounds a greedy step of transformers' generate): per generated token
+    # every weight once (GPT-2-small: 124M parameters, the tied wte doubling as lm_head) + the visible K and V of every
+    # layer; the prefill's reads are counted as one step.  The step is host-launch bound at batch 1 (~100 kernels of
+    # microseconds each), so the fraction is small; it is the number to hold against the reference's own batch-1 path.
+    n_par = sum(p.numel() for p in gpu_model.parameters())
+    kv_key = 2 * cfg.n_layer * cfg.n_embd * 2
+    new_t = gen["max_new_tokens"]
+    tot_bytes = sum(new_t * n_par * 2 + kv_key * sum(ids.shape[1] + t for t in range(new_t)) for ids, _ in prompts)
+    roof = {"bound": "hbm", "achieved": round(tot_bytes / gpu_s / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(tot_bytes / gpu_s / 1e9 / PEAK_HBM_GBS, 5), "traffic": None,
+            "kernel": "whole batch-1 greedy decode (transformers generate with the cram_hip attention: prefill_kernel "
+                      "/ decode_kernel d = 64, library GEMMs)",
+            "bytes_per_question": tot_bytes / len(prompts),
+            "note": "algorithmic bytes = weights once per generated token + visible K/V; batch 1 as the reference "
+                    "(re_weighting.py:40), launch-bound"}
     print(json.dumps({
         "metric": METRIC + " [config 1: GPT-2-small reweighted decode]", "value": round(value, 3),
         "unit": "questions/s", "n_gpus": 1, "steps": args.steps, "warmup": 1, "ms_per_step": round(gpu_s * 1e3, 2),
@@ -681,7 +726,7 @@ def run_config1(args):
         "config": {"workload": "GPT-2-small, 8 NQ questions x 5 retrieved docs, batch-1 hooked-decode shape, all "
                                "heads re-weighted, 32 new tokens",
                    "mean_prompt_tokens": round(T_mean, 1), "parallelism": "single GPU, batch 1"},
-        "roofline": None, "cpu_baseline": cpu,
+        "roofline": roof, "cpu_baseline": cpu,
         "speedup_vs_cpu": round(value / cpu["value"], 1) if cpu else None}), flush=True)
 
 

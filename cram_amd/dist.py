@@ -44,17 +44,21 @@ def env_rank() -> Tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
-def init(backend: Optional[str] = None) -> Tuple[int, int, int]:
+def init(backend: Optional[str] = None, timeout_min: float = 30.0) -> Tuple[int, int, int]:
+    """Join the process group of a torch.distributed.run launch.  timeout_min bounds every collective's wait: the
+    bench's rank 0 times the CPU hook path (minutes) while the other ranks wait at the final barrier."""
+    import datetime
     rank, world, local = env_rank()
     if world > 1 and not dist.is_initialized():
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        to = datetime.timedelta(minutes=timeout_min)
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dist.init_process_group(backend, device_id=torch.device("cuda", local), timeout=to)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=to)
     return rank, world, local
 
 
@@ -113,15 +117,18 @@ def gather_rows(local: torch.Tensor, local_ids: torch.Tensor, n_total: int, grou
     row = 1
     for s in local.shape[1:]:
         row *= int(s)
-    buf = torch.zeros((kmax, row + 1), dtype=torch.float64, device=dev)
+    # one id column in front of the row; fp32 IE rows travel as fp32 (ids < 2^24 are exact in fp32: NQ-1000 x 32
+    # layers = 32,000 rows), anything else as fp64
+    wire = torch.float32 if local.dtype == torch.float32 and n_total < (1 << 24) else torch.float64
+    buf = torch.zeros((kmax, row + 1), dtype=wire, device=dev)
     buf[:, 0] = -1
-    buf[:local.shape[0], 0] = local_ids.to(dev, torch.float64)
-    buf[:local.shape[0], 1:] = local.reshape(local.shape[0], row).double()   # a rank may hold no rows
-    allb = torch.empty((world * kmax, row + 1), dtype=torch.float64, device=dev)
+    buf[:local.shape[0], 0] = local_ids.to(dev, wire)
+    buf[:local.shape[0], 1:] = local.reshape(local.shape[0], row).to(wire)   # a rank may hold no rows
+    allb = torch.empty((world * kmax, row + 1), dtype=wire, device=dev)
     dist.all_gather_into_tensor(allb, buf, group=group)
     keep = allb[:, 0] >= 0
     ids = allb[keep, 0].long()
-    out = torch.zeros((n_total, row), dtype=torch.float64, device=dev)
+    out = torch.zeros((n_total, row), dtype=wire, device=dev)
     out[ids] = allb[keep, 1:]
     return out.reshape((n_total,) + tuple(local.shape[1:])).to(device=home, dtype=local.dtype)
 

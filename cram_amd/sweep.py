@@ -176,7 +176,9 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     lw = eng.layers[l]
     hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
     hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
-    with _modes(eng, qc.exact, False):
+    # row-exact: the variant batches run every row on the 4-wave kernel too (no split-K tail), so every variant row
+    # rounds as the baseline's does (the tail's rows used to sum their K ranges in another order)
+    with _modes(eng, qc.exact, qc.exact):
         h, x2 = eng.o_proj_norm(abuf, lw, hin)                         # [Mp, D]
         h, m = eng.mlp_residual(x2, lw, h)                              # layer output h (+ m when deferred)
         if not last:
@@ -236,33 +238,66 @@ def _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_pref
     return out
 
 
-def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None, base_variant: bool = False) -> float:
-    """Algorithmic GEMM+attention flops of ie_question(layers=...) (for roofline accounting): one baseline
-    forward plus the suffix work of every swept layer; p0 = skipped prefix rows; base_variant: the batches carry
-    the un-perturbed variant (not row-exact)."""
-    L, H, d, D = spec.num_layers, spec.num_heads, spec.head_dim, spec.hidden
-    Hv = H + 1 if base_variant else H
+def _flop_parts(spec):
+    """Per-row GEMM flops of one decoder layer by part: (q, k | v, o_proj + MLP), and the attention count."""
+    D, F = spec.hidden, spec.intermediate
+    fq = 2.0 * D * spec.q_size
+    fkv = 2.0 * D * 2 * spec.kv_size
+    frest = 2.0 * (spec.q_size * D + 3 * D * F)
 
-    def attn(tq, s):   # tq queries at positions s-tq .. s-1, causal
+    def attn(tq, s):   # tq queries at positions s-tq .. s-1, causal: QK^T + PV over the visible keys
         vis = tq * (s - tq) + tq * (tq + 1) / 2.0
-        return 4.0 * d * spec.num_heads * vis
+        return 4.0 * spec.head_dim * spec.num_heads * vis
+    return fq, fkv, frest, attn
 
-    lay = lambda t: spec.layer_flops(t)
-    qkv_frac = (spec.q_size + 2 * spec.kv_size) * D / ((spec.q_size + 2 * spec.kv_size) * D + spec.q_size * D
-                                                      + 3 * D * spec.intermediate)
+
+def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None) -> float:
+    """ALGORITHMIC GEMM + attention flops of ie_question(layers=...) -- the work the IE of SURVEY §8(d) needs, the
+    step roofline's numerator: one baseline forward plus, per swept layer l, the all-heads-biased attention of
+    layer l and H = num_heads variant batches (head h of layer l re-weighted) through o_proj + MLP of layer l and
+    the layers above.  Rows before p0 (the first biased key) are equal in every variant and are not recomputed
+    (prefix skip).  The last layer of every forward needs K / V of every row but q, attention, o_proj and MLP of the
+    n answer rows only.  What the sweep executes beyond this (the un-perturbed 33rd variant of the default mode, the
+    GEMMs' pad rows, the baseline's last-layer q over every row) is sweep_flops_executed()."""
+    L, H = spec.num_layers, spec.num_heads
+    fq, fkv, frest, attn = _flop_parts(spec)
     p0 = max(0, min(p0, T - n_ans))
     Ts = T - p0
-    f = 0.0
-    # baseline: L-1 full layers + last layer (qkv over T, rest over n)
-    f += (L - 1) * (lay(T) + attn(T, T)) + qkv_frac * lay(T) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T)
+    lay = fq + fkv + frest
+    last_layer = lambda t: fkv * t + (fq + frest) * n_ans + attn(n_ans, t)   # K/V of every row, the rest on n rows
+    # baseline: L-1 full layers + the last layer
+    f = (L - 1) * (lay * T + attn(T, T)) + last_layer(T)
+    for l in (range(L) if layers is None else layers):
+        rows = n_ans if l == L - 1 else Ts
+        f += attn(rows, T)                                              # all-heads-biased attention of layer l
+        f += H * frest * rows                                           # o_proj + MLP of layer l, H variants
+        for l2 in range(l + 1, L):
+            f += H * (fkv * Ts + (fq + frest) * n_ans + attn(n_ans, T) if l2 == L - 1
+                      else lay * Ts + attn(Ts, T))
+    return f
+
+
+def sweep_flops_executed(spec, T: int, n_ans: int, p0: int = 0, layers=None, base_variant: bool = True) -> float:
+    """The GEMM + attention flops ie_question EXECUTES: sweep_flops plus the un-perturbed variant each batch carries
+    (base_variant: the default, not row-exact mode), the pad rows of the suffix layers' GEMMs (engine.padded_rows:
+    the 256-row macro tile, then the measured row table) and the baseline forward's last-layer q over every row."""
+    from .engine import padded_rows
+    L, H = spec.num_layers, spec.num_heads
+    Hv = H + 1 if base_variant else H
+    fq, fkv, frest, attn = _flop_parts(spec)
+    p0 = max(0, min(p0, T - n_ans))
+    Ts = T - p0
+    lay = fq + fkv + frest
+    Mp = padded_rows(Hv * Ts, spec)                                     # GEMM rows of a suffix batch
+    f = (L - 1) * (lay * T + attn(T, T)) + (fq + fkv) * T + frest * n_ans + attn(n_ans, T)
     for l in (range(L) if layers is None else layers):
         last = l == L - 1
         rows = n_ans if last else Ts
-        f += attn(rows, T)                                              # all-heads biased attention
-        f += Hv * (1 - qkv_frac) * lay(rows)                            # o_proj + MLP of layer l, Hv variants
+        f += attn(rows, T)
+        f += frest * (Hv * n_ans if last else Mp)                       # o_proj + MLP of layer l over the batch
         for l2 in range(l + 1, L):
             if l2 == L - 1:
-                f += Hv * (qkv_frac * lay(Ts) + (1 - qkv_frac) * lay(n_ans) + attn(n_ans, T))
+                f += fkv * Mp + (fq + frest) * Hv * n_ans + Hv * attn(n_ans, T)
             else:
-                f += Hv * (lay(Ts) + attn(Ts, T))
+                f += lay * Mp + Hv * attn(Ts, T)
     return f

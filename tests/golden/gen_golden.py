@@ -20,6 +20,8 @@ Outputs (data only) in tests/golden/:
   llama2_*.json.gz  G4/G4'/G5/G6 for the fp16 MHA Llama-2 stand-in (`python gen_golden.py llama2`): the reference's
                     default model family, loaded as fp16 by torch_dtype="auto"; its "bf16" IE variant holds the
                     model-dtype (fp16) logits
+  qwen2_gqa7_*.json.gz G4/G4'/G6 for the Qwen2 GQA-7 kind (`python gen_golden.py gqa7`): 7 q-heads per kv head and
+                    q/k/v bias as in Qwen2-7B, 4 layers x 14 heads (2 kv heads), 12 NQ questions
 """
 import contextlib
 import gzip
@@ -296,6 +298,11 @@ def main():
         gen_ie_f32(rw, (("llama2", 3),), "llama2_ie_f32.json.gz")
         gen_generate(rw, (("llama2", {0: [1], 2: [0, 3]}), ("llama2", {})), "llama2_generate.json.gz")
         gen_logprobs(rw, ("llama2",), "llama2_logprobs.json.gz")
+    if "gqa7" in which:
+        # Qwen2-7B's GQA-7 grouping with q/k/v bias, 4 layers x 14 heads (56 IE values per question)
+        gen_ie(rw, (("qwen2_gqa7", 12),), "qwen2_gqa7_ie.json.gz")
+        gen_ie_f32(rw, (("qwen2_gqa7", 12),), "qwen2_gqa7_ie_f32.json.gz")
+        gen_logprobs(rw, ("qwen2_gqa7",), "qwen2_gqa7_logprobs.json.gz")
 
 
 if __name__ == "__main__":

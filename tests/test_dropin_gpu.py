@@ -40,7 +40,20 @@ def nq():
 @pytest.fixture(scope="module")
 def paths(tmp_path_factory):
     root = str(tmp_path_factory.mktemp("tiny"))
-    return {k: tm.save_model(k, root) for k in ("llama3", "qwen2")}
+    return {k: tm.save_model(k, root) for k in ("llama3", "qwen2", "qwen2_gqa7")}
+
+
+# golden files per kind: (IE grids, IE of the float32 copy, answer log-probs); the GQA-7 kind has its own
+def _gold_files(kind):
+    if kind == "qwen2_gqa7":
+        return "qwen2_gqa7_ie.json.gz", "qwen2_gqa7_ie_f32.json.gz", "qwen2_gqa7_logprobs.json.gz"
+    return "tiny_ie.json.gz", "tiny_ie_f32.json.gz", "logprobs.json.gz"
+
+
+def _first3(agg_all, kind, ie_err, ref_err, idx):
+    """The original three Qwen2 questions (idx 0-2) as their own logged aggregate."""
+    if kind == "qwen2" and idx < 3:
+        agg_all.setdefault("first3", parity.Aggregate()).ie_errors(ie_err, ref_err, subset="qwen2 idx 0-2", idx=idx)
 
 
 @pytest.fixture(scope="module")
@@ -60,12 +73,18 @@ def test_spans_on_device(fbh):
         assert w[0].float().tolist() == r["weight"]
 
 
-@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+def _sub_errors(ie, ref, truth):
+    ie, ref, truth = (np.asarray(x, dtype=np.float64) for x in (ie, ref, truth))
+    return np.abs(ie - truth), np.abs(ref - truth)
+
+
+@pytest.mark.parametrize("kind", ["llama3", "qwen2", "qwen2_gqa7"])
 def test_cal_logits_matches_reference(fbh, nq, kind):
-    gold = [x for x in _load("tiny_ie.json.gz") if x["kind"] == kind and x["variant"] == "fp32"]
-    truth = {x["idx"]: x["ie"] for x in _load("tiny_ie_f32.json.gz") if x["kind"] == kind}
+    f_ie, f_truth, _ = _gold_files(kind)
+    gold = [x for x in _load(f_ie) if x["kind"] == kind and x["variant"] == "fp32"]
+    truth = {x["idx"]: x["ie"] for x in _load(f_truth) if x["kind"] == kind}
     obj = fbh[kind]
-    agg = parity.Aggregate()
+    agg, sub = parity.Aggregate(), {}
     for g in gold:
         rec = nq[g["idx"]]
         ie = obj.cal_logits(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
@@ -73,24 +92,36 @@ def test_cal_logits_matches_reference(fbh, nq, kind):
         assert isinstance(ie, list) and len(ie) == obj.model_num_hidden_layers
         assert all(isinstance(v, float) for v in ie[0])
         ie_tolerance_check(ie, g["ie"], truth[g["idx"]], agg)
+        _first3(sub, kind, *_sub_errors(ie, g["ie"], truth[g["idx"]]), g["idx"])
+    if kind == "qwen2_gqa7":                         # >= 6 questions whose IE is not identically 0
+        assert agg.informative("ie_max") >= 6
     agg.check()
+    for a in sub.values():
+        a.log_aggregates()
 
 
-@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+@pytest.mark.parametrize("kind", ["llama3", "qwen2", "qwen2_gqa7"])
 def test_cal_logits_bf16_logits_match_reference(fbh, nq, kind):
     """round_logits=True (each answer logit rounded to the model dtype, as transformers 5.15 returns them) against
     the reference run under the same convention (G4 'bf16' variant, re_weighting.py:159-160,170), same bar."""
-    gold = [x for x in _load("tiny_ie.json.gz") if x["kind"] == kind and x["variant"] == "bf16"]
-    truth = {x["idx"]: x["ie"] for x in _load("tiny_ie_f32.json.gz") if x["kind"] == kind}
+    f_ie, f_truth, _ = _gold_files(kind)
+    gold = [x for x in _load(f_ie) if x["kind"] == kind and x["variant"] == "bf16"]
+    truth = {x["idx"]: x["ie"] for x in _load(f_truth) if x["kind"] == kind}
     assert gold
     obj = fbh[kind]
-    agg = parity.Aggregate()
+    agg, sub = parity.Aggregate(), {}
     for g in gold:
         rec = nq[g["idx"]]
         ie = obj.cal_logits_tensor(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"],
                                    scores=[0, 1, 1, 1, 1], wrong_answer=rec["wrong_answer"], round_logits=True)
-        ie_tolerance_check(ie.double().cpu().numpy(), g["ie"], truth[g["idx"]], agg)
+        ie = ie.double().cpu().numpy()
+        ie_tolerance_check(ie, g["ie"], truth[g["idx"]], agg)
+        _first3(sub, kind, *_sub_errors(ie, g["ie"], truth[g["idx"]]), g["idx"])
+    if kind == "qwen2_gqa7":
+        assert agg.informative("ie_max") >= 6
     agg.check()
+    for a in sub.values():
+        a.log_aggregates()
 
 
 def test_cal_logits_deterministic(fbh, nq):
@@ -255,13 +286,13 @@ def test_batched_sweep_equals_unbatched_on_gpu(fbh, nq):
     assert np.abs(sw - un).max() < 0.05, np.abs(sw - un).max()
 
 
-@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+@pytest.mark.parametrize("kind", ["llama3", "qwen2", "qwen2_gqa7"])
 def test_answer_logprobs_match_reference_hook(paths, nq, gpu_device, kind):
     """G6: re-weighted answer-token log-probabilities through the drop-in (transformers model + cram_hip
     attention) vs the reference hook path.  Bar: per token |ours - fp32 truth| <= 2.5 x the reference's own
     bf16 error on that sample + 0.01 (truth = the reference hook on the float32 copy of the weights)."""
     from cram_amd.re_weighting import Re_Weighting_Strategy
-    rows = [r for r in _load("logprobs.json.gz") if r["kind"] == kind]
+    rows = [r for r in _load(_gold_files(kind)[2]) if r["kind"] == kind]
     truth = {(r["idx"], r["scores"], r["heads"]): np.array(r["logprobs"]) for r in rows if r["fp32"]}
     objs = {}
     worst = 0.0

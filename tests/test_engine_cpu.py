@@ -345,12 +345,63 @@ def test_fp32_truth_batched_grid_equals_per_unit(tiny, nq):
     assert (grid - per).abs().max() < 1e-4 * max(1.0, per.abs().max().item())
 
 
+def _ie_flops_by_enumeration(sp, T, n, p0):
+    """Independent count of the IE sweep's algorithmic work (SURVEY §8(d) with the prefix skip): every weight matrix
+    of every layer applied to the rows that need it, attention by summing each query row's visible keys."""
+    D, F, d = sp.hidden, sp.intermediate, sp.head_dim
+    mats = {"q": (sp.q_size, D), "k": (sp.kv_size, D), "v": (sp.kv_size, D), "o": (D, sp.q_size),
+            "gate": (F, D), "up": (F, D), "down": (D, F)}
+
+    def gemm(names, rows):
+        return sum(2 * mats[m][0] * mats[m][1] * rows for m in names)
+
+    memo = {}
+
+    def attn(q_rows):                         # query rows at absolute positions q_rows, causal over keys 0..i
+        if q_rows not in memo:
+            memo[q_rows] = sum(4 * d * sp.num_heads * (i + 1) for i in q_rows)
+        return memo[q_rows]
+
+    L, H = sp.num_layers, sp.num_heads
+    everything, rest = list(mats), ["o", "gate", "up", "down"]
+    suffix, answer = range(p0, T), range(T - n, T)
+    f = 0
+    for l in range(L):                         # the un-hooked forward
+        if l < L - 1:
+            f += gemm(everything, T) + attn(range(T))
+        else:                                  # K / V of every row, the rest for the answer rows
+            f += gemm(["k", "v"], T) + gemm(["q"] + rest, n) + attn(answer)
+    for l in range(L):                         # per hooked layer: the all-heads-biased attention, then H variants
+        rows = answer if l == L - 1 else suffix
+        f += attn(rows)
+        for _h in range(H):
+            f += gemm(rest, len(rows))
+            for l2 in range(l + 1, L):
+                if l2 == L - 1:
+                    f += gemm(["k", "v"], len(suffix)) + gemm(["q"] + rest, n) + attn(answer)
+                else:
+                    f += gemm(everything, len(suffix)) + attn(suffix)
+    return f
+
+
 def test_sweep_flops_accounting():
+    """sweep_flops (the step roofline's numerator) equals an independent enumeration of SURVEY §8(d)'s work with the
+    prefix skip (32 variants, the last layer's q / attention / MLP on the answer rows); what the sweep executes on top
+    (the un-perturbed variant, pad rows) is sweep_flops_executed, reported beside it."""
     from cram_amd.engine import ModelSpec
     sp = ModelSpec.llama3_8b()
-    f = sweep.sweep_flops(sp, 904, 4)
+    for T, n, p0 in ((904, 4, 25), (907, 3, 0), (962, 5, 37)):
+        f = sweep.sweep_flops(sp, T, n, p0)
+        assert f == pytest.approx(_ie_flops_by_enumeration(sp, T, n, p0), rel=1e-12)
+        ex = sweep.sweep_flops_executed(sp, T, n, p0)
+        # the 33rd variant adds ~1/32 of the variant work; pad rows at most +2048 GEMM rows per batch
+        assert 1.025 * f < ex < 1.12 * f
+        assert sweep.sweep_flops_executed(sp, T, n, p0, base_variant=False) < ex
+    small = ModelSpec(3, 256, 4, 2, 128, 512, 1000, 1e-5, False, "llama")
+    assert sweep.sweep_flops(small, 97, 3, 11) == pytest.approx(_ie_flops_by_enumeration(small, 97, 3, 11), rel=1e-12)
+    assert sweep.sweep_flops(small, 97, 3, 11, layers=[2]) < sweep.sweep_flops(small, 97, 3, 11, layers=[0])
     ref_fwd = 2 * (6.98e9 + 0.525e9) * 904          # one reference-style full forward
-    assert 0.3 * 1025 * ref_fwd < f < 0.6 * 1025 * ref_fwd
+    assert 0.3 * 1025 * ref_fwd < sweep.sweep_flops(sp, 904, 4) < 0.6 * 1025 * ref_fwd
 
 
 @pytest.mark.parametrize("family", ["llama", "qwen2"])

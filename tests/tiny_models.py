@@ -22,8 +22,9 @@ TOK_DIR = {"llama3": os.path.join(REPO, "data", "tok_llama3"), "qwen2": os.path.
 # names select the reference's chat branch; "gpt2-tiny" and "Llama-2-tiny" match neither, i.e. the
 # raw-template branch (the reference's default model, Llama-2-13b-chat-hf, takes that branch too)
 DIR_NAME = {"llama3": "Llama-3-tiny", "qwen2": "Qwen2-tiny", "gpt2": "gpt2-tiny", "llama2": "Llama-2-tiny",
-            "qwen2_7b": "Qwen2-7B-heads-2layer"}
+            "qwen2_7b": "Qwen2-7B-heads-2layer", "qwen2_gqa7": "Qwen2-GQA7-tiny"}
 TOK_DIR["qwen2_7b"] = TOK_DIR["qwen2"]
+TOK_DIR["qwen2_gqa7"] = TOK_DIR["qwen2"]
 DTYPE = {"llama2": torch.float16}
 
 SPECS = {
@@ -44,9 +45,16 @@ SPECS = {
     "qwen2_7b": dict(hidden_size=3584, intermediate_size=18944, num_hidden_layers=2, num_attention_heads=28,
                      num_key_value_heads=4, rope_theta=1000000.0, rms_norm_eps=1e-6,
                      max_position_embeddings=4096, tie_word_embeddings=False),
+    # Qwen2-7B's head grouping (7 q-heads per kv head, head_dim 128, q/k/v bias, rope 1e6) at 4 layers x 14 heads
+    # (2 kv heads): 56 IE values per question (the 3 x 2 "qwen2" kind has 6), the GQA-7 attention kernels and every
+    # fused GEMM epilogue (widths as Qwen2-7B's: hidden a multiple of 256, an even q/k/v head count) on the
+    # reference-pinned path
+    "qwen2_gqa7": dict(hidden_size=1792, intermediate_size=2048, num_hidden_layers=4, num_attention_heads=14,
+                       num_key_value_heads=2, rope_theta=1000000.0, rms_norm_eps=1e-6,
+                       max_position_embeddings=4096, tie_word_embeddings=False),
 }
-# linear-weight std per kind (fan-in 256 for the tiny kinds; the full-width kind keeps the activations O(1))
-LIN_STD_KIND = {"qwen2_7b": 0.02}
+# linear-weight std per kind (fan-in 256 for the tiny kinds; wider kinds keep the activations O(1): std ~ 1.3/sqrt(fan-in))
+LIN_STD_KIND = {"qwen2_7b": 0.02, "qwen2_gqa7": 0.03}
 SEED = 20250404
 LIN_STD = 0.08
 

@@ -28,7 +28,7 @@ PYT="python -u -m pytest tests -m gpu --timeout 300 --timeout-method thread"
 for step in "$@"; do
   echo "== $step ($(date +%T))"
   case "$step" in
-    suite)     timeout -k 10 1000 $PYT -x -v > $O/gputest.txt 2>&1; tail -3 $O/gputest.txt ;;
+    suite)     timeout -k 10 1000 $PYT -x -v --durations=60 > $O/gputest.txt 2>&1; tail -3 $O/gputest.txt ;;
     suite-all) timeout -k 10 1000 $PYT -v > $O/gputest.txt 2>&1 || echo "pytest rc=$?"; tail -5 $O/gputest.txt ;;
     smoke)     timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1
                tail -2 $O/smoke.txt ;;
