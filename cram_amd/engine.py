@@ -703,8 +703,11 @@ class DecodeSession:
         # 116.6 us for hipBLASLt + cram_silu_mul at 512 rows; it loses at 129 rows (86 vs 64) and on Qwen2's shape
         # (N 37,888, K 3,584: 167.8 vs 153.1; config 4 steps 13.9 -> 14.5 ms), profiles/r04/dec129/, decq/; the
         # interleaved weight is built here, outside the step graph
+        # CRAM_DECODE_MLP_W4=1 / 0 forces it on / off at any shape the kernel takes (A/B of other shapes)
+        w4_env = os.environ.get("CRAM_DECODE_MLP_W4", "auto")
         self.mlp_w4 = (not self.splits_gemm["gu"] and self.B >= DECODE_MLP_W4_MIN_ROWS and eng.device.type == "cuda"
-                       and (2 * sp.intermediate, sp.hidden) == (28672, 4096)     # the measured shape only
+                       and ((2 * sp.intermediate, sp.hidden) == (28672, 4096) if w4_env == "auto"   # measured shape
+                            else w4_env == "1")
                        and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))
                        and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         # gate/up where the 4-wave kernel's 256 x 256 tiles spill just past one wave of the CUs (Qwen2-7B at 512 rows:
@@ -825,28 +828,41 @@ class DecodeSession:
 
     def _prefill_prefix(self, p: int):
         """The shared prefix once (rows 0..p-1 of prompt 0: causal, unbiased), its K/V of every layer into cache row
-        0, then copied to every other row."""
+        0, then copied to every other row.  The projections run on the packed prefill's kernels whatever the prefix's
+        row count (q/k/v + RoPE into the cache, o_proj / down_proj + residual, gate/up + SiLU-mul on the 4-wave GEMM,
+        which rounds a row the same whatever M): the prefix rows' K/V then differ from a whole-prompt prefill's only
+        where the attention kernel's 32-row blocks fall differently."""
         eng, sp = self.eng, self.eng.spec
         h = eng.embed[self.prompts[0][:p]]
         m = None
-        for l, lw in enumerate(eng.layers):
-            if m is None:
-                x = ops.rmsnorm(h, lw.ln1, sp.eps)
-            else:
-                h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
-            y = ops.linear(x, lw.wqkv, lw.bqkv)
-            ops.rope_split(y, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, p,
-                           self.k_cache[l][:1].transpose(1, 2), self.v_cache[l][:1].transpose(1, 2), 0, keep_k=True)
-            self.k_cache[l][1:, :, :p] = self.k_cache[l][:1, :, :p]
-            self.v_cache[l][1:, :, :p] = self.v_cache[l][:1, :, :p]
-            if l == sp.num_layers - 1:              # the last layer's K/V are all the prefix contributes
-                break
-            q = y[:, :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))[None]
-            k = y[:, sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))[None]
-            v = y[:, sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))[None]
-            a = eng.attention(q, k, v)
-            h, x2 = ops.rmsnorm(ops.linear(a.reshape(p, sp.q_size), lw.wo), lw.ln2, sp.eps, residual=h)
-            m = eng.mlp(x2, lw)
+        prev = eng.fused_any_rows, eng.no_tail_split
+        eng.fused_any_rows, eng.no_tail_split = True, True
+        try:
+            for l, lw in enumerate(eng.layers):
+                if m is None:
+                    x = ops.rmsnorm(h, lw.ln1, sp.eps)
+                else:
+                    h, x = ops.rmsnorm(m, lw.ln1, sp.eps, residual=h)
+                kc, vc = self.k_cache[l][:1].transpose(1, 2), self.v_cache[l][:1].transpose(1, 2)
+                if eng._fused_qkv_ok(x, lw):
+                    y = ops.gemm_rope(x, lw.wqkv, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, p,
+                                      rows=p, kout=kc, vout=vc, row0=0, keep_k=True, bias=lw.bqkv)
+                else:
+                    y = ops.linear(x, lw.wqkv, lw.bqkv)
+                    ops.rope_split(y, sp.num_heads, sp.num_kv_heads, sp.head_dim, self.cos, self.sin, p, kc, vc, 0,
+                                   keep_k=True)
+                self.k_cache[l][1:, :, :p] = self.k_cache[l][:1, :, :p]
+                self.v_cache[l][1:, :, :p] = self.v_cache[l][:1, :, :p]
+                if l == sp.num_layers - 1:              # the last layer's K/V are all the prefix contributes
+                    break
+                q = y[:, :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))[None]
+                k = y[:, sp.q_size:sp.q_size + sp.kv_size].unflatten(-1, (sp.num_kv_heads, sp.head_dim))[None]
+                v = y[:, sp.q_size + sp.kv_size:].unflatten(-1, (sp.num_kv_heads, sp.head_dim))[None]
+                a = eng.attention(q, k, v)
+                h, x2 = eng.o_proj_norm(a.reshape(p, sp.q_size), lw, h)
+                h, m = eng.mlp_residual(x2, lw, h)
+        finally:
+            eng.fused_any_rows, eng.no_tail_split = prev
 
     def prefill(self, max_rows: int = PREFILL_CHUNK_ROWS):
         """All prompts in packed varlen passes of at most ``max_rows`` tokens each (GEMM M = the chunk's token

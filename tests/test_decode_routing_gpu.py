@@ -208,7 +208,15 @@ def test_shared_prefix_prefill_at_llama3_widths(l3w, monkeypatch):
     assert s0.prefix == 0
     for c, c0 in ((s.k_cache, s0.k_cache), (s.v_cache, s0.v_cache)):
         a, b = c[:, :, :, :p].float(), c0[:, :, :, :p].float()
-        assert (a - b).abs().max() <= 0.05 * b.abs().max() + 0.05, (a - b).abs().max()
+        # layer 0: the prefix runs the packed prefill's own GEMM kernels (row-independent): bit-equal
+        assert torch.equal(c[0, :, :, :p], c0[0, :, :, :p])
+        # above it only the attention kernel's 32-row blocks fall differently (prefix alone vs whole prompt)
+        d = (a - b).abs()
+        eq = float((a == b).float().mean())
+        print(f"\nprefix K/V vs whole-prompt prefill: max |diff| {d.max():.3e} (max |x| {b.abs().max():.2f}), "
+              f"mean |diff| {d.mean():.3e}, equal {eq:.4f}")
+        assert d.max() <= 0.02 * b.abs().max() + 0.02, d.max()
+        assert eq >= 0.9, eq
     whole = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
     monkeypatch.setattr(E, "PREFIX_SHARE", True)
     shared = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)

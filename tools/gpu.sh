@@ -16,6 +16,7 @@
 #   pmcgemm          the dominant GEMM launch's PMC passes (tools/pmc_gemm.sh) -> gemm_pmc_summary.txt + gemm_pmc.json
 #   test:PATTERN     pytest -m gpu -k PATTERN
 #   py:SCRIPT,ARGS   python SCRIPT ARGS (a probe under tools/)
+#   pyt:SEC:SCRIPT,ARGS  the same under a time limit of SEC seconds
 set -e
 set -o pipefail
 export TMPDIR=/tmp
@@ -53,6 +54,8 @@ for step in "$@"; do
                timeout -k 10 900 $PYT -x -v -s -k "$k" > $O/test_$n.txt 2>&1; tail -3 $O/test_$n.txt ;;
     py:*)      a=${step#py:}; n=$(basename "${a%%,*}" .py)$(echo "${a#*,}" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
                timeout -k 10 600 python -u ${a//,/ } > $O/$n.txt 2>&1; tail -30 $O/$n.txt ;;
+    pyt:*)     a=${step#pyt:}; lim=${a%%:*}; a=${a#*:}; n=$(basename "${a%%,*}" .py)$(echo "${a#*,}" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
+               timeout -k 10 $lim python -u ${a//,/ } > $O/$n.txt 2>&1; tail -30 $O/$n.txt ;;
     *)         echo "unknown step $step"; exit 2 ;;
   esac
 done
