@@ -55,7 +55,7 @@ def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, i
     def run():
         ops.attn_decode(q, sess.k_cache[0], sess.v_cache[0], scale=eng.scale, seq_lens=sess.seq_lens,
                         bias=sess.cb.bias, enable=sess.cb.enable[0], W=sess.cb.W, num_splits=sess.splits,
-                        workspace=sess.ws, out=out)
+                        workspace=sess.ws, out=out, shared_rows=sess.shared_read)
 
     for _ in range(3):
         run()
@@ -67,7 +67,9 @@ def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, i
     e.record(st)
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / iters
-    kv_bytes = float(sum(sess.lens)) * sp.num_kv_heads * sp.head_dim * 2 * 2
+    # visible K/V rows; the batch's shared opening (whole 32-key blocks, read from cache row 0) counted once
+    sh = sess.shared_read // 32 * 32
+    kv_bytes = float(sum(sess.lens) - (sess.B - 1) * sh) * sp.num_kv_heads * sp.head_dim * 2 * 2
     ach = kv_bytes / (ms * 1e-3) / 1e9
     G = sp.num_heads // sp.num_kv_heads
     kern = ("decode_mfma_kernel (16x16x32 matrix cores, GQA group of %d)" % G if G >= 4 and sp.head_dim == 128
@@ -75,6 +77,7 @@ def decode_attention_roofline(eng, prompts, weights16, heads, new_tokens, dev, i
     res = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None, "kernel": kern,
            "avg_launch_ms": round(ms, 4), "bytes_per_launch": kv_bytes, "batch": sess.B, "splits": sess.splits,
+           "shared_rows_read_once": sh,
            "note": "layer 0 of the decode leg's prefilled KV cache, timed apart from the decode leg"}
     del sess
     torch.cuda.empty_cache()
@@ -90,7 +93,8 @@ def decode_leg_roofline(spec, phases, dtype):
                the batch's shared prefix (DecodeSession.shared_prefix, computed once) are counted once;
       steps    HBM-bound: per greedy step, every weight once (L layers' projections + lm_head, the embedding is a
                B-row gather) + every row's visible K and V (L * Hkv * d * 2 tensors * 2 B per key, the keys growing
-               by one per step) over the steps' time, against 8 TB/s (6.3 achievable)."""
+               by one per step; the batch's shared opening, read from one cache row, once) over the steps' time,
+               against 8 TB/s (6.3 achievable)."""
     import torch  # noqa: F401
     L, D, V = spec.num_layers, spec.hidden, spec.vocab
     esz = 2
@@ -110,8 +114,9 @@ def decode_leg_roofline(spec, phases, dtype):
         pf_ms += ph["t0"].elapsed_time(ph["prefill"])
         cap_ms += ph["prefill"].elapsed_time(ph["capture"])
         st_ms += ph["capture"].elapsed_time(ph["steps"])
+        shr = ph.get("shared_read", 0) * (len(lens) - 1)       # the shared opening's rows, read once per step
         for t in range(1, ph["n_steps"] + 1):
-            st_bytes += w_bytes + kv_per_key * sum(T + t for T in lens)
+            st_bytes += w_bytes + kv_per_key * (sum(T + t for T in lens) - shr)
         n_steps += ph["n_steps"]
     pf = pf_flops / (pf_ms * 1e-3) / 1e12
     bw = st_bytes / (st_ms * 1e-3) / 1e9

@@ -17,7 +17,7 @@ _c_int32_p = POINTER(ctypes.c_int32)
 _c_uint8_p = POINTER(ctypes.c_uint8)
 _c_float_p = POINTER(c_float)
 
-ABI_VERSION = 7   # CRAM_ABI_VERSION of include/cram_attn.h
+ABI_VERSION = 8   # CRAM_ABI_VERSION of include/cram_attn.h
 
 # name -> (restype, argtypes); the exact export list of include/cram_attn.h
 SIGNATURES = {
@@ -53,6 +53,16 @@ SIGNATURES = {
         c_int, c_int, c_int, c_int, c_void_p, c_int, c_float,
         c_void_p, c_int64, c_void_p, c_int64, c_int,
         c_int, c_void_p, c_size_t,
+        c_int, c_void_p,
+    ]),
+    "cram_attn_decode_shared": (c_int, [
+        c_void_p, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64, c_int64,
+        c_void_p, c_int64, c_int64,
+        c_int, c_int, c_int, c_int, c_void_p, c_int, c_float,
+        c_void_p, c_int64, c_void_p, c_int64, c_int,
+        c_int, c_int, c_void_p, c_size_t,
         c_int, c_void_p,
     ]),
     "cram_answer_logits": (c_int, [

@@ -612,6 +612,8 @@ struct DecodeParams {
   float scale_log2;
   float* ws_o;   // [B][Hq][nsplit][D] unnormalised partial outputs (split mode)
   float* ws_ml;  // [B][Hq][nsplit][2]  partial (max, sum)
+  int shared;    // keys [0, shared) are equal in every batch row (a shared prompt opening, copied into each row): the
+                 // matrix-core body reads them from batch row 0 (one HBM stream for the batch); a multiple of 32
 };
 
 template <typename T, int D, int G, int U = 4>   // U: keys per lane group per iteration
@@ -836,6 +838,14 @@ __global__ __launch_bounds__(256, 2) void decode_mfma_kernel(DecodeParams p) {
                                                       0x00020000);
   const float* brow = p.bias ? p.bias + b * p.bias_sb : nullptr;
   const auto bsrd = __builtin_amdgcn_make_buffer_rsrc((void*)brow, (short)0, en_any ? p.W * 4 : 0, 0x00020000);
+  // the shared opening's rows from batch row 0 (same bits as this row's copy; every row's workgroups read one copy)
+  const int shared = min(p.shared, k_end) & ~(KB - 1);
+  const T* kbase0 = static_cast<const T*>(p.k) + hkv * p.k_sh;
+  const T* vbase0 = static_cast<const T*>(p.v) + hkv * p.v_sh;
+  const auto ksrd0 = __builtin_amdgcn_make_buffer_rsrc((void*)kbase0, (short)0,
+                                                       (int)(max(shared - 1, 0) * p.k_st * 2 + D * 2), 0x00020000);
+  const auto vsrd0 = __builtin_amdgcn_make_buffer_rsrc((void*)vbase0, (short)0,
+                                                       (int)(max(shared - 1, 0) * p.v_st * 2 + D * 2), 0x00020000);
 
   // per-lane constant offsets
   uint32_t koff[2][4];   // K: row (16 hh + q), bytes 64 c + 16 g
@@ -853,14 +863,17 @@ __global__ __launch_bounds__(256, 2) void decode_mfma_kernel(DecodeParams p) {
   f32x4 bn[2];
   auto load_block = [&](int blk) {
     const int key0 = k_begin + blk * KB;
+    const bool sh = key0 + KB <= shared;                 // wave-uniform
+    const auto kd = sh ? ksrd0 : ksrd;
+    const auto vd = sh ? vsrd0 : vsrd;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        kn[hh][c] = __builtin_amdgcn_raw_buffer_load_b128(ksrd, (int)(koff[hh][c] + key0 * p.k_st * 2), 0, 0);
+        kn[hh][c] = __builtin_amdgcn_raw_buffer_load_b128(kd, (int)(koff[hh][c] + key0 * p.k_st * 2), 0, 0);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      vn[i] = __builtin_amdgcn_raw_buffer_load_b128(vsrd, (int)(vrow_off + (key0 + 4 * i) * p.v_st * 2), 0, 0);
+      vn[i] = __builtin_amdgcn_raw_buffer_load_b128(vd, (int)(vrow_off + (key0 + 4 * i) * p.v_st * 2), 0, 0);
     if (en_any) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
@@ -1304,7 +1317,18 @@ int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh, const void* k, i
                      int64_t o_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d, float scale,
                      const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
                      int num_splits, void* workspace, size_t workspace_bytes, int dtype, cram_stream_t stream) {
-  if (!q || !k || !v || !o) return CRAM_ERR_INVALID_ARG;
+  return cram_attn_decode_shared(q, q_sb, q_sh, k, k_sb, k_sh, k_st, v, v_sb, v_sh, v_st, o, o_sb, o_sh, B, Hq, Hkv,
+                                 S, seq_lens, d, scale, bias, bias_sb, enable, en_sb, W, 0, num_splits, workspace,
+                                 workspace_bytes, dtype, stream);
+}
+
+int cram_attn_decode_shared(const void* q, int64_t q_sb, int64_t q_sh, const void* k, int64_t k_sb, int64_t k_sh,
+                            int64_t k_st, const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st, void* o,
+                            int64_t o_sb, int64_t o_sh, int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d,
+                            float scale, const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb,
+                            int W, int shared_rows, int num_splits, void* workspace, size_t workspace_bytes, int dtype,
+                            cram_stream_t stream) {
+  if (!q || !k || !v || !o || shared_rows < 0) return CRAM_ERR_INVALID_ARG;
   if (B <= 0 || Hq <= 0 || Hkv <= 0 || S <= 0 || Hq % Hkv != 0 || num_splits <= 0 || B > 65535 ||
       num_splits > 65535)
     return CRAM_ERR_INVALID_ARG;
@@ -1324,6 +1348,7 @@ int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh, const void* k, i
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.S = S; p.W = bias ? W : 0;
   p.scale_log2 = scale * kLog2e;
   p.ws_o = nullptr; p.ws_ml = nullptr;
+  p.shared = shared_rows & ~31;
   if (num_splits > 1) {
     const size_t need = cram_attn_decode_workspace_size(B, Hq, d, num_splits);
     if (!workspace || workspace_bytes < need || !al16(workspace)) return CRAM_ERR_WORKSPACE;

@@ -103,6 +103,9 @@ LAST_Q_ROWS_ONLY = os.environ.get("CRAM_LAST_Q_ROWS", "1") != "0"
 # CRAM_PREFIX_SHARE=0 prefills whole prompts (A/B, tests).
 PREFIX_SHARE = os.environ.get("CRAM_PREFIX_SHARE", "1") != "0"
 PREFIX_SHARE_MIN_ROWS = 16
+# ... and the decode attention reads those rows from cache row 0 (cram_attn_decode_shared: one HBM stream of the
+# opening per step instead of one per row, bit-identical); CRAM_SHARED_DECODE_READ=0 reads every row's copy (A/B)
+SHARED_DECODE_READ = os.environ.get("CRAM_SHARED_DECODE_READ", "1") != "0"
 
 
 def padded_rows(M: int, spec: Optional["ModelSpec"] = None) -> int:
@@ -544,6 +547,7 @@ class CrAMEngine:
             phases["n_steps"] = n_steps
             phases["lens"] = list(sess.lens)
             phases["prefix"] = int(getattr(sess, "prefix", 0))
+            phases["shared_read"] = int(sess.shared_read) // 32 * 32      # rows the step's attention reads once
         out = []
         gen = sess.generated().cpu().tolist()
         for row in gen:
@@ -687,6 +691,7 @@ class DecodeSession:
         self.ws = (torch.empty(ops.decode_workspace_bytes(self.B, sp.num_heads, sp.head_dim, self.splits),
                                dtype=torch.uint8, device=dev) if self.splits > 1 else None)
         self.graph = None
+        self.prefix = self.shared_read = 0          # set by prefill(): the batch's shared opening
         self.rows = torch.arange(self.B, device=dev)
         self.cos, self.sin = eng.rope_tables(self.S_max)
         # split-K plan of the step's projections (0 = F.linear) and one workspace shared by all of them (the
@@ -873,6 +878,7 @@ class DecodeSession:
         host stall per call)."""
         b0 = 0
         self.prefix = p = self.shared_prefix()
+        self.shared_read = p if SHARED_DECODE_READ else 0
         with gemm_tune.pinned():
             if p:
                 self._prefill_prefix(p)
@@ -931,7 +937,8 @@ class DecodeSession:
                 # other rows' last-layer outputs are never read: 2.7 % of the prefill's FLOPs)
                 a = ops.attn_decode(q[last], self.k_cache[l][b0:b1], self.v_cache[l][b0:b1], scale=eng.scale,
                                     seq_lens=self.seq_lens[b0:b1], bias=bias, enable=self.cb.enable[l, b0:b1],
-                                    W=self.cb.W, num_splits=self.splits, workspace=self.ws)
+                                    W=self.cb.W, num_splits=self.splits, workspace=self.ws,
+                                    shared_rows=self.shared_read)
                 h, x2 = ops.rmsnorm(ops.linear(a.flatten(-2), lw.wo), lw.ln2, sp.eps, residual=h[last])
                 m = eng.mlp(x2, lw)
                 break
@@ -969,9 +976,10 @@ class DecodeSession:
                            self.k_cache[l].transpose(1, 2), self.v_cache[l].transpose(1, 2), 0, pos=self.pos,
                            dst_b=self.rows)
             q = y[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
+            # the batch's shared opening (prefilled once, copied into every row) read from row 0 (bit-identical)
             a = ops.attn_decode(q[:, 0], self.k_cache[l], self.v_cache[l], scale=eng.scale, seq_lens=self.seq_lens,
                                 bias=self.cb.bias, enable=self.cb.enable[l], W=self.cb.W, num_splits=self.splits,
-                                workspace=self.ws)
+                                workspace=self.ws, shared_rows=self.shared_read)
             h, x2 = eng.add_rmsnorm(self._proj(a.flatten(-2)[:, None], lw.wo, None, "o"), h, lw.ln2)
             m = self._mlp(x2, lw)
         _, hn = eng.add_rmsnorm(m[:, 0], h[:, 0], eng.norm)

@@ -243,12 +243,14 @@ def decode_workspace_bytes(B: int, Hq: int, d: int, num_splits: int) -> int:
 def attn_decode(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: float,
                 seq_lens: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
                 enable: Optional[torch.Tensor] = None, W: int = 0, num_splits: int = 1,
-                workspace: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                workspace: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                shared_rows: int = 0) -> torch.Tensor:
     """Single-token attention.  q [B, Hq, d]; k/v [B, Hkv, S_max, d]; out [B, Hq, d].
 
     ``seq_lens`` (int32 [B], device) gives the number of valid keys per row
     (default: all S_max).  ``num_splits`` > 1 needs ``workspace`` (uint8, at
-    least ``decode_workspace_bytes`` bytes).
+    least ``decode_workspace_bytes`` bytes).  ``shared_rows`` > 0: keys / values [0, shared_rows) are equal in
+    every batch row (the caller's guarantee); they are read from row 0 (cram_attn_decode_shared, same results).
     """
     _check16("q", q, 3)
     _check16("k", k, 4, q)
@@ -269,14 +271,16 @@ def attn_decode(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, *, scale: flo
         if workspace is None:
             workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
         ws_ptr, ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
-    code = lib.cram_attn_decode(
+    if shared_rows < 0 or shared_rows > S:
+        raise ValueError("shared_rows must be in [0, S_max]")
+    code = lib.cram_attn_decode_shared(
         q.data_ptr(), q.stride(0), q.stride(1),
         k.data_ptr(), k.stride(0), k.stride(1), k.stride(2),
         v.data_ptr(), v.stride(0), v.stride(1), v.stride(2),
         out.data_ptr(), out.stride(0), out.stride(1),
         B, Hq, Hkv, S, _ptr(seq_lens), d, float(scale),
-        bp, bsb, ep, esb, W, int(num_splits), ws_ptr, ws_bytes, _dt(q), _stream(q.device))
-    _lib.check(code, "cram_attn_decode")
+        bp, bsb, ep, esb, W, int(shared_rows), int(num_splits), ws_ptr, ws_bytes, _dt(q), _stream(q.device))
+    _lib.check(code, "cram_attn_decode_shared")
     return out
 
 

@@ -48,10 +48,11 @@ extern "C" {
 #define CRAM_ERR_LAUNCH -4        /* hipLaunchKernel failed */
 #define CRAM_ERR_WORKSPACE -5     /* split-S workspace missing or too small */
 
-#define CRAM_ABI_VERSION 7        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
+#define CRAM_ABI_VERSION 8        /* 2: dtype argument on every tensor entry point; 3: kernel-selection knobs;
                                      4: cram_get_knob(which, *value), decode projection GEMM;
                                      5: cram_gemm_residual, cram_gemm_rope, cram_gemm_splitk_residual;
-                                     6: cram_gemm_small; 7: cram_attn_prefill_varlen_cached */
+                                     6: cram_gemm_small; 7: cram_attn_prefill_varlen_cached;
+                                     8: cram_attn_decode_shared */
 
 #define CRAM_DTYPE_BF16 0
 #define CRAM_DTYPE_F16 1
@@ -157,6 +158,22 @@ int cram_attn_decode(const void* q, int64_t q_sb, int64_t q_sh,
                      const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
                      int num_splits, void* workspace, size_t workspace_bytes,
                      int dtype, cram_stream_t stream);
+
+/*
+ * (ABI 8) cram_attn_decode for a batch whose rows share their first `shared_rows` keys (the prompt opening prefilled
+ * once and copied into every cache row, cram_attn_prefill_varlen_cached): the caller guarantees keys / values
+ * [0, shared_rows) are equal in every batch row; the matrix-core body then reads them (in whole 32-key blocks) from
+ * batch row 0, one HBM stream for the batch instead of one per row.  Results are bit-identical to cram_attn_decode.
+ * shared_rows = 0 is cram_attn_decode.
+ */
+int cram_attn_decode_shared(const void* q, int64_t q_sb, int64_t q_sh,
+                            const void* k, int64_t k_sb, int64_t k_sh, int64_t k_st,
+                            const void* v, int64_t v_sb, int64_t v_sh, int64_t v_st,
+                            void* o, int64_t o_sb, int64_t o_sh,
+                            int B, int Hq, int Hkv, int S, const int32_t* seq_lens, int d, float scale,
+                            const float* bias, int64_t bias_sb, const uint8_t* enable, int64_t en_sb, int W,
+                            int shared_rows, int num_splits, void* workspace, size_t workspace_bytes,
+                            int dtype, cram_stream_t stream);
 
 /*
  * Answer-token logits (replaces the full-vocab lm_head + gather of

@@ -39,7 +39,7 @@ def attn_prefill(q, k, v, *, scale, q_pos0=None, bias=None, enable=None, W=0, ou
 
 
 def attn_decode(q, k, v, *, scale, seq_lens=None, bias=None, enable=None, W=0, num_splits=1, workspace=None,
-                out=None):
+                out=None, shared_rows=0):
     B, Hq, d = q.shape
     outs = []
     for b in range(B):

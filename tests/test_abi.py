@@ -16,7 +16,7 @@ def _declared():
 
 def test_header_declares_the_boundary():
     names = _declared()
-    for n in ("cram_attn_prefill", "cram_attn_decode", "cram_attn_decode_workspace_size", "cram_answer_logits",
+    for n in ("cram_attn_prefill", "cram_attn_decode", "cram_attn_decode_shared", "cram_attn_decode_workspace_size", "cram_answer_logits",
               "cram_strerror", "cram_abi_version", "cram_rmsnorm", "cram_rope_inplace", "cram_rope_split", "cram_silu_mul",
               "cram_gemm", "cram_gemm_residual", "cram_gemm_rope"):
         assert n in names
@@ -30,7 +30,7 @@ def test_library_builds_loads_and_exports_every_symbol():
         assert hasattr(lib, n), n
     assert set(_declared()) == set(_lib.SIGNATURES), "ctypes signatures must cover the header exactly"
     L = _lib.load()
-    assert L.cram_abi_version() == _lib.ABI_VERSION == 7
+    assert L.cram_abi_version() == _lib.ABI_VERSION == 8
     assert L.cram_strerror(-3) == b"stride not a multiple of 8 elements or pointer not 16-byte aligned"
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 4) == 2 * 32 * 4 * 130 * 4
     assert L.cram_attn_decode_workspace_size(2, 32, 128, 1) == 0

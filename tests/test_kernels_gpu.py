@@ -114,6 +114,35 @@ def test_decode_matches_oracle(gpu_device, decode_variant, B, Hq, Hkv, S, d, spl
     _check(out, ref)
 
 
+@pytest.mark.parametrize("B,Hq,Hkv,S,shared,splits", [
+    (5, 32, 8, 900, 37, 1), (3, 32, 8, 900, 64, 2), (4, 28, 4, 777, 40, 1), (3, 28, 4, 777, 96, 3),
+    (2, 32, 8, 120, 31, 1), (3, 8, 8, 300, 64, 2)])
+def test_decode_shared_rows_bit_identical(gpu_device, decode_variant, B, Hq, Hkv, S, shared, splits):
+    """cram_attn_decode_shared (ABI 8): with keys / values [0, shared) equal in every batch row (the decode batch's
+    shared opening, copied into each cache row), reading them from row 0 gives the same bits as reading each row's
+    copy; ragged lengths, bias, split-S, GQA 4 / 7 (matrix-core body) and MHA (VALU body, which ignores it)."""
+    from cram_amd import ops
+    dev = gpu_device
+    gen = torch.Generator().manual_seed(S + shared + splits)
+    q = torch.randn(B, Hq, 128, generator=gen).to(torch.bfloat16).to(dev)
+    k = torch.randn(B, Hkv, S + 5, 128, generator=gen).to(torch.bfloat16).to(dev)
+    v = torch.randn(B, Hkv, S + 5, 128, generator=gen).to(torch.bfloat16).to(dev)
+    k[1:, :, :shared] = k[:1, :, :shared]
+    v[1:, :, :shared] = v[:1, :, :shared]
+    lens = torch.tensor([max(shared + 1, S - 9 * b) for b in range(B)], dtype=torch.int32, device=dev)
+    _, bias, enable, _ = _bias_inputs(B, Hq, S, S - 2, gen)
+    kw = dict(scale=128 ** -0.5, seq_lens=lens, bias=bias.to(dev), enable=enable.to(dev), W=S - 2, num_splits=splits)
+    a = ops.attn_decode(q, k, v, **kw)
+    b = ops.attn_decode(q, k, v, shared_rows=shared, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    # the indirection is real: poisoning the other rows' copies of whole shared 32-key blocks changes nothing
+    if shared >= 32 and Hq // Hkv >= 4 and decode_variant == "auto":
+        k[1:, :, :shared // 32 * 32] = 0
+        c = ops.attn_decode(q, k, v, shared_rows=shared, **kw)
+        assert torch.equal(a, c)
+
+
 def test_answer_logits(gpu_device):
     gen = torch.Generator().manual_seed(3)
     n, D, V = 37, 4096, 1000
