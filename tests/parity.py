@@ -46,9 +46,9 @@ class Aggregate:
         self.sums = {}
 
     def add(self, family: str, ours: float, ref: float, **extra) -> None:
-        """One sample.  A 0/0 sample (both errors exactly 0: e.g. a question whose passage spans the tokenizer does
-        not locate, so the sweep's bias is empty and every IE is 0 in every run) carries no information: it is
-        logged but counts neither in the aggregate nor in its sample count n."""
+        """One sample.  A 0/0 sample (both errors exactly 0: a question whose wrong answer is ONE token, so the
+        reference's answer ids -- first id dropped, re_weighting.py:155 -- are empty and every IE is 0 in every run)
+        carries no information: it is logged but counts neither in the aggregate nor in its sample count n."""
         ours, ref = float(ours), float(ref)
         informative = ours != 0.0 or ref != 0.0
         record(family, ours, ref, informative=informative, **extra)

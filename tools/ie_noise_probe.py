@@ -79,6 +79,8 @@ def main():
             i = g["idx"]
             rec = nq[i]
             paras = rec["ori_fake"] + rec["reranked_dense_ctxs"]
+            if fbh.answer_ids(rec["wrong_answer"]).numel() == 0:      # one-token answer: IE == 0 in every run
+                continue
             kw = dict(question=rec["question"], paras=paras, scores=[0, 1, 1, 1, 1], wrong_answer=rec["wrong_answer"])
             grids = {"golden": np.array(g["ie"])}
             grids["sweep"] = fbh.cal_logits_tensor(**kw).double().cpu().numpy()
