@@ -124,6 +124,55 @@ def test_cal_logits_bf16_logits_match_reference(fbh, nq, kind):
         a.log_aggregates()
 
 
+def test_qwen2_ie_against_reference_executions(fbh, paths, nq, gpu_device):
+    """The tiny Qwen2's first three questions (our IE max error 1.6-1.9x the fixture's on idx 0 and 2).
+    The fixture is ONE execution of the reference code (CPU, transformers sdpa); other valid bf16 executions of the
+    same unmodified algorithm -- the dense-mask hook on transformers' GPU sdpa and eager attention (oracle/hook_ref.py,
+    bit-exact to re_weighting.py on CPU) -- land 0.07-0.12 from the float32 truth on those questions, where the CPU
+    sdpa draw landed 0.036-0.039 (tools/ie_noise_probe.py, profiles/r06/ie_noise.jsonl).  The reference's own error
+    is therefore measured here as the mean over the three executions, and ours (the sweep) must stay within 1.3x of it
+    over the three questions, mean and max of |IE - truth| (the original per-fixture bar is
+    test_cal_logits_matches_reference's)."""
+    from transformers import AutoModelForCausalLM
+    from oracle import hook_ref
+    gold = {x["idx"]: x["ie"] for x in _load("tiny_ie.json.gz") if x["kind"] == "qwen2" and x["variant"] == "fp32"}
+    truth = {x["idx"]: np.array(x["ie"]) for x in _load("tiny_ie_f32.json.gz") if x["kind"] == "qwen2"}
+    obj = fbh["qwen2"]
+    models = [AutoModelForCausalLM.from_pretrained(paths["qwen2"], dtype=torch.bfloat16,
+                                                   attn_implementation=impl).eval().to(gpu_device)
+              for impl in ("sdpa", "eager")]
+    tot = {"ours_mean": 0.0, "ours_max": 0.0, "ref_mean": 0.0, "ref_max": 0.0}
+    for i in range(3):
+        rec = nq[i]
+        paras = rec["ori_fake"] + rec["reranked_dense_ctxs"]
+        ours = np.array(obj.cal_logits(question=rec["question"], paras=paras, scores=[0, 1, 1, 1, 1],
+                                       wrong_answer=rec["wrong_answer"]))
+        enc, w = obj.decode_with_special_attention(question=rec["question"], paras=paras, scores=[0, 1, 1, 1, 1],
+                                                   answer=rec["wrong_answer"])
+        ans = obj.answer_ids(rec["wrong_answer"]).to(gpu_device)
+        runs = [np.array(gold[i])]
+        for m in models:
+            h = m.lm_head.register_forward_hook(
+                lambda mod, a, o: torch.nn.functional.linear(a[0].float(), mod.weight.float()))
+            try:
+                runs.append(hook_ref.ie_grid(m, enc["input_ids"], hook_ref.log_weight(w).to(gpu_device), ans))
+            finally:
+                h.remove()
+        t = truth[i]
+        e_ref = [np.abs(r - t) for r in runs]
+        e_o = np.abs(ours - t)
+        tot["ours_mean"] += e_o.mean()
+        tot["ours_max"] += e_o.max()
+        tot["ref_mean"] += float(np.mean([e.mean() for e in e_ref]))
+        tot["ref_max"] += float(np.mean([e.max() for e in e_ref]))
+        parity.record("ie_max", e_o.max(), float(np.mean([e.max() for e in e_ref])), idx=i,
+                      reference="mean of 3 executions", executions=[float(e.max()) for e in e_ref])
+    for fam in ("mean", "max"):
+        parity.record(f"ie_{fam}_aggregate", tot[f"ours_{fam}"], tot[f"ref_{fam}"], samples=3,
+                      reference="mean of 3 executions")
+        assert tot[f"ours_{fam}"] <= 1.3 * tot[f"ref_{fam}"], (fam, tot)
+
+
 def test_cal_logits_deterministic(fbh, nq):
     rec = nq[3]
     args = dict(question=rec["question"], paras=rec["ori_fake"] + rec["reranked_dense_ctxs"], scores=[0, 1, 1, 1, 1],
