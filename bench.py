@@ -169,6 +169,8 @@ def main():
     # projections run near the matrix-core rate, M = 256 ones at 1.5-4 TB/s of weights); the KV cache of 512 rows is
     # 69 GB of the 288 GB (round 3: 72.4 vs 67.9 questions/s at 256 on one box, profiles/r03/s5_probe1/)
     ap.add_argument("--decode-batch", type=int, default=512)
+    ap.add_argument("--kv-frac", type=float, default=0.55,
+                    help="fraction of HBM the decode KV cache may take (rows per batch = this / bytes per row)")
     ap.add_argument("--decode-tokens", type=int, default=100, help="new tokens per question (re_weighting.py:127)")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--scores", default="ideal", choices=["ideal", "gpt"],
@@ -363,12 +365,13 @@ def main():
         encs = spans.encode_batch(tok, name, qs, ps, ss)                     # host: prompts -> ids + fp16 weights
         host_ms = (time.perf_counter() - th) * 1e3
         lens = [ids.numel() for ids, _, _ in encs]
-        # the static KV cache is [L][B][Hkv][S_max][d] for K and V: rows per batch = what fits in 0.55 of HBM next
-        # to the weights and the packed-prefill activations (config 5: ~1.1 GB per 8.4k-token row -> ~128 rows;
-        # MHA Llama-2-13b: 0.9 GB per 1.1k-token row)
+        # the static KV cache is [L][B][Hkv][S_max][d] for K and V: rows per batch = what fits in --kv-frac of HBM
+        # next to the weights (16 GB + the 7.5 GB interleaved gate/up) and the packed-prefill activations (32k-row
+        # chunks, a few GB) (config 5: ~1.1 GB per 8.4k-token row -> 128 rows; MHA Llama-2-13b: 0.9 GB per
+        # 1.1k-token row)
         s_max = max(lens) + args.decode_tokens
         per_row = 2 * spec.num_layers * spec.num_kv_heads * s_max * spec.head_dim * 2
-        cap = max(1, int(0.55 * torch.cuda.get_device_properties(dev).total_memory // per_row))
+        cap = max(1, int(args.kv_frac * torch.cuda.get_device_properties(dev).total_memory // per_row))
         # whole 64-row groups when the budget binds: the decode step's projections run on 128-row tiles
         # (cram_gemm_small), so one row past a multiple of 128 would cost a whole extra tile (config 5: 129 -> 128)
         cap = cap // 64 * 64 if cap >= 128 else cap

@@ -45,6 +45,7 @@ from .engine import CrAMEngine, padded_rows
 # over 13 full grids its IE error and k = 894 overlap equal the default's, but it fails the frozen
 # grid bar on that test's question (a ~1-sigma bar), so the default keeps the variant.
 ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "0") == "1"
+EXACT_TAIL_SPLIT = os.environ.get("CRAM_ROW_EXACT_TAIL_SPLIT", "0") == "1"
 
 
 class QuestionCache:
@@ -177,8 +178,9 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
     hin[:M].view(Hv, rows, sp.hidden).copy_(qc.h_in[l][:, -rows:].expand(Hv, rows, sp.hidden))
     # row-exact: the variant batches run every row on the 4-wave kernel too (no split-K tail), so every variant row
-    # rounds as the baseline's does (the tail's rows used to sum their K ranges in another order)
-    with _modes(eng, qc.exact, qc.exact):
+    # rounds as the baseline's does (the tail's rows used to sum their K ranges in another order);
+    # CRAM_ROW_EXACT_TAIL_SPLIT=1 keeps the split-K tail in the variant batches (A/B of its cost)
+    with _modes(eng, qc.exact, qc.exact and not EXACT_TAIL_SPLIT):
         h, x2 = eng.o_proj_norm(abuf, lw, hin)                         # [Mp, D]
         h, m = eng.mlp_residual(x2, lw, h)                              # layer output h (+ m when deferred)
         if not last:

@@ -215,8 +215,9 @@ def test_shared_prefix_prefill_at_llama3_widths(l3w, monkeypatch):
         eq = float((a == b).float().mean())
         print(f"\nprefix K/V vs whole-prompt prefill: max |diff| {d.max():.3e} (max |x| {b.abs().max():.2f}), "
               f"mean |diff| {d.mean():.3e}, equal {eq:.4f}")
-        assert d.max() <= 0.02 * b.abs().max() + 0.02, d.max()
-        assert eq >= 0.9, eq
+        # measured: max 3.1e-2 (one bf16 ulp at |x| ~ 6), 98.4 % of the elements equal (profiles/r06/)
+        assert d.max() <= 0.01 * b.abs().max() + 0.01, d.max()
+        assert eq >= 0.95, eq
     whole = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
     monkeypatch.setattr(E, "PREFIX_SHARE", True)
     shared = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)

@@ -166,10 +166,10 @@ def test_qwen2_ie_against_reference_executions(fbh, paths, nq, gpu_device):
         tot["ref_mean"] += float(np.mean([e.mean() for e in e_ref]))
         tot["ref_max"] += float(np.mean([e.max() for e in e_ref]))
         parity.record("ie_max", e_o.max(), float(np.mean([e.max() for e in e_ref])), idx=i,
-                      reference="mean of 3 executions", executions=[float(e.max()) for e in e_ref])
+                      reference_kind="mean of 3 executions", executions=[float(e.max()) for e in e_ref])
     for fam in ("mean", "max"):
         parity.record(f"ie_{fam}_aggregate", tot[f"ours_{fam}"], tot[f"ref_{fam}"], samples=3,
-                      reference="mean of 3 executions")
+                      reference_kind="mean of 3 executions")
         assert tot[f"ours_{fam}"] <= 1.3 * tot[f"ref_{fam}"], (fam, tot)
 
 

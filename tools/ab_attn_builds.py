@@ -35,8 +35,9 @@ def call(lib, q, k, v, out, bias, enable, W):
 
 
 def main():
-    paths = sys.argv[1:3]
-    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+    args = sys.argv[1:]
+    rounds = int(args.pop()) if args and args[-1].isdigit() else 7
+    paths = args                                   # the first is the base; every other is timed against it
     libs = [load(p) for p in paths]
     dev = torch.device("cuda:0")
     d = 128
@@ -63,8 +64,10 @@ def main():
         for lib, o in zip(libs, outs):
             call(lib, q, k, v, o, bias, enable, W)
         torch.cuda.synchronize()
-        dmax = (outs[0].float() - outs[1].float()).abs().max().item()
-        print(f"{name}: max |A - B| = {dmax:.3e}", flush=True)
+        for i in range(1, len(libs)):
+            dmax = (outs[0].float() - outs[i].float()).abs().max().item()
+            print(f"{name}: max |{paths[0].rsplit('/', 1)[-1]} - {paths[i].rsplit('/', 1)[-1]}| = {dmax:.3e}",
+                  flush=True)
     res = {(i, c[0]): [] for i in range(len(libs)) for c in cases}
     for _ in range(rounds):
         for i, lib in enumerate(libs):
@@ -82,9 +85,9 @@ def main():
         B, T, _b, p0 = name
         fl, _ = ops.prefill_work(B, 32, 8, T, T + p0, d, p0)
         ms = [statistics.median(res[(i, name)]) for i in range(len(libs))]
-        print(f"{str(name):22s} A {ms[0]:.3f} ms {fl / ms[0] / 1e9:6.0f} TF ({fl / ms[0] / 2.5e12:.3f})  "
-              f"B {ms[1]:.3f} ms {fl / ms[1] / 1e9:6.0f} TF ({fl / ms[1] / 2.5e12:.3f})  B/A speed {ms[0] / ms[1]:.3f}x",
-              flush=True)
+        print(f"{str(name):22s} " + "  ".join(
+            f"{paths[i].rsplit('/', 1)[-1]} {ms[i]:.3f} ms {fl / ms[i] / 1e9:6.0f} TF ({fl / ms[i] / 2.5e12:.3f})"
+            + ("" if i == 0 else f" {ms[0] / ms[i]:.3f}x") for i in range(len(libs))), flush=True)
 
 
 if __name__ == "__main__":

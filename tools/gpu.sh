@@ -17,6 +17,7 @@
 #   test:PATTERN     pytest -m gpu -k PATTERN
 #   py:SCRIPT,ARGS   python SCRIPT ARGS (a probe under tools/)
 #   pyt:SEC:SCRIPT,ARGS  the same under a time limit of SEC seconds
+#   dist2:ARGS       bench.py ARGS at N = 2 (torch.distributed.run, gloo, both ranks on the one GPU)
 set -e
 set -o pipefail
 export TMPDIR=/tmp
@@ -54,6 +55,12 @@ for step in "$@"; do
                timeout -k 10 900 $PYT -x -v -s -k "$k" > $O/test_$n.txt 2>&1; tail -3 $O/test_$n.txt ;;
     py:*)      a=${step#py:}; n=$(basename "${a%%,*}" .py)$(echo "${a#*,}" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
                timeout -k 10 600 python -u ${a//,/ } > $O/$n.txt 2>&1; tail -30 $O/$n.txt ;;
+    dist2:*)   a=${step#dist2:}; n=$(echo "$a" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
+               # the bench's N = 2 path rehearsed on the one GPU: two gloo ranks share the device (RCCL refuses two
+               # ranks on one GPU), torch.distributed.run as the driver launches it
+               timeout -k 10 900 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+                 --master-port 29533 bench.py --gpus 2 --dist-backend gloo ${a//,/ } > $O/dist2_$n.json 2> $O/dist2_$n.err
+               head -c 700 $O/dist2_$n.json; echo ;;
     pyt:*)     a=${step#pyt:}; lim=${a%%:*}; a=${a#*:}; n=$(basename "${a%%,*}" .py)$(echo "${a#*,}" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
                timeout -k 10 $lim python -u ${a//,/ } > $O/$n.txt 2>&1; tail -30 $O/$n.txt ;;
     *)         echo "unknown step $step"; exit 2 ;;

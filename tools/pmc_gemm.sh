@@ -17,6 +17,12 @@ run p2 SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INS
 run p3 FETCH_SIZE
 run p4 WRITE_SIZE
 run p5 TCC_HIT_sum TCC_MISS_sum SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32
+if [ "${EXTRA:-0}" = 1 ]; then
+  # the L2's fabric read requests by size (what FETCH_SIZE is derived from) and by destination, written requests:
+  # a direct byte count of the beyond-L2 traffic, independent of FETCH_SIZE's gfx950 correction
+  run p6 TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
+  run p7 TCC_EA0_RDREQ_DRAM_32B_sum TCC_EA0_RDREQ_GMI_32B_sum TCC_BUBBLE_sum TCC_EA0_WRREQ_64B_sum
+fi
 for f in $OUT/p*/p*_counter_collection.csv; do echo "== $f"; python3 - "$f" <<'PY'
 import csv, sys, collections
 rows = list(csv.DictReader(open(sys.argv[1])))

@@ -106,6 +106,18 @@ def main():
                  "mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); effective clock = "
                  f"GRBM_GUI_ACTIVE / 8 / wall; mfma issues x {MFMA_FLOP} FLOP / algorithmic FLOPs"),
     }
+    if "TCC_EA0_RDREQ_128B_sum" in c:
+        # request-size passes (EXTRA=1 tools/pmc_gemm.sh): beyond-L2 read bytes counted from the requests themselves
+        n32, n64, n128 = (mean(c[f"TCC_EA0_RDREQ_{w}B_sum"]) for w in (32, 64, 128))
+        req_b = 32 * n32 + 64 * n64 + 128 * n128
+        out["rdreq_bytes"] = req_b
+        out["rdreq_counts"] = {"all": mean(c["TCC_EA0_RDREQ_sum"]), "32B": n32, "64B": n64, "128B": n128}
+        out["rdreq_bytes_over_fetch_size_x2"] = round(req_b / read_b, 4)
+        out["traffic_by_request_sizes_over_algorithmic"] = round((req_b + write_b) / alg_bytes, 4)
+        if "TCC_EA0_RDREQ_DRAM_32B_sum" in c:
+            out["rdreq_dram_bytes"] = 32 * mean(c["TCC_EA0_RDREQ_DRAM_32B_sum"])
+            out["rdreq_gmi_bytes"] = 32 * mean(c["TCC_EA0_RDREQ_GMI_32B_sum"])
+            out["tcc_bubble_128B"] = mean(c["TCC_BUBBLE_sum"])
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
