@@ -165,11 +165,12 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5])
-    # max rows per decode batch.  NQ-1000 on one GPU = two batches of 500: 512 prompts per GPU share every decode step's 15 GB weight read (the M = 512
-    # projections run near the matrix-core rate, M = 256 ones at 1.5-4 TB/s of weights); the KV cache of 512 rows is
-    # 69 GB of the 288 GB (round 3: 72.4 vs 67.9 questions/s at 256 on one box, profiles/r03/s5_probe1/)
-    ap.add_argument("--decode-batch", type=int, default=512)
-    ap.add_argument("--kv-frac", type=float, default=0.55,
+    # max rows per decode batch.  Round 6: NQ-1000 on one GPU in ONE batch of 1000 rows (KV cache ~180 GB of the 288
+    # GB: --kv-frac 0.68): every decode step's 15 GB weight read and its projections serve all 1000 rows, 34.2 ms per
+    # step against 2 x 18.8 for two batches of 500 -- 81.8 vs 79.5 questions/s on one box (profiles/r06/decode_b*.json;
+    # round 3 moved 256 -> 512 rows: 72.4 vs 67.9)
+    ap.add_argument("--decode-batch", type=int, default=1024)
+    ap.add_argument("--kv-frac", type=float, default=0.68,
                     help="fraction of HBM the decode KV cache may take (rows per batch = this / bytes per row)")
     ap.add_argument("--decode-tokens", type=int, default=100, help="new tokens per question (re_weighting.py:127)")
     ap.add_argument("--no-decode", action="store_true")

@@ -567,7 +567,7 @@ class CrAMEngine:
 # profiles/r03/decode_gemm_probe_*.jsonl): only the long-K down projection wins (Llama-3 N 4096 x K 14336: 55.9 vs
 # 62.9 us at 8 ranges = 128 workgroups); at K <= N (q/k/v, o_proj, gate/up, lm_head) the fp32 partial slabs and
 # their combine cost more than the library loses, so those stay on F.linear.  CRAM_DECODE_GEMM=0 turns it off (A/B).
-DECODE_GEMM_MAX_ROWS = 512
+DECODE_GEMM_MAX_ROWS = int(os.environ.get("CRAM_DECODE_GEMM_MAX_ROWS", "512"))   # A/B override
 DECODE_GEMM_TARGET_WGS = 128
 DECODE_GEMM_MIN_K_OVER_N = 2
 DECODE_QKV_SPLIT_MAX_ROWS = 192
