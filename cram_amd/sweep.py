@@ -17,16 +17,17 @@ Here, per question:
   4. answer logits come from the fp32 gather-dot kernel (no full vocab);
   5. IE stays on the device; one host copy per question (or one all-gather).
 Noise cancellation: in the reference, ori and cur share bit-identical arithmetic
-for every layer below the hooked one (re_weighting.py:159 vs :169).  By default
-each layer's batch carries one un-perturbed variant (first) and IE[l, h] = its
-sum - variant h's, so ori and cur round alike below and beside the perturbation.
-In the opt-in row-exact mode the same holds by construction: the baseline forward
-runs every projection on the kernels the variant batches run (the 4-wave GEMM
-whatever the row count, no split-K tail), its attention over the suffix rows
-[p0, T) as one call of the shape the variants' calls have, so an un-perturbed
-row computes the same bits in the baseline as in any variant batch, and
-IE[l, h] = ori(baseline) - sum over variant h (not where the fused kernels do not
-apply: the CPU stand-ins, widths the epilogues do not take).
+for every layer below the hooked one (re_weighting.py:159 vs :169).  In the
+row-exact mode (the default since round 6) that holds by
+construction: the baseline forward and the variant batches run every projection on
+the same kernel (the 4-wave GEMM whatever the row count, no split-K tail, whose
+per-element accumulation order does not depend on M or on the row's place), the
+baseline's attention over the suffix rows [p0, T) as one call of the shape the
+variants' calls have, so an un-perturbed row computes the same bits in the baseline
+as in any variant batch, and IE[l, h] = ori(baseline) - sum over variant h.  Where
+the fused kernels do not apply (the CPU stand-ins, widths the epilogues do not take;
+CRAM_SWEEP_ROW_EXACT=0) each layer's batch carries one un-perturbed variant (first)
+and IE[l, h] = its sum - variant h's, so ori and cur round alike.
 Work per question: L*H*(L-1)/2 + ... layer-forwards instead of (1 + L*H) * L.
 """
 from __future__ import annotations
@@ -41,10 +42,14 @@ from . import gemm_tune, ops
 from .bias import CredibilityBias
 from .engine import CrAMEngine, padded_rows
 
-# Opt-in (CRAM_SWEEP_ROW_EXACT=1): drop the un-perturbed variant where the arithmetic is row-exact.  +2.1 % heads/s;
-# over 13 full grids its IE error and k = 894 overlap equal the default's, but it fails the frozen
-# grid bar on that test's question (a ~1-sigma bar), so the default keeps the variant.
-ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "0") == "1"
+# Row-exact sweep (the default since round 6; CRAM_SWEEP_ROW_EXACT=0 carries the un-perturbed variant in every batch):
+# the baseline forward rounds every un-perturbed row as the variant batches do, so no batch carries an un-perturbed
+# variant (1/33 of the work).  It passes the multi-question full-grid bars of tests/test_fullsize_ie_gpu.py over 13
+# NQ questions (RMS error vs the float32 truth 0.943x the reference algorithm's own, k = 894 overlap -1.7 against a
+# -13.8 bar; the carried-variant mode: 0.930x, -2.2), +1.7 % heads/s (profiles/r06/)
+ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "1") == "1"
+# CRAM_ROW_EXACT_TAIL_SPLIT=1: the variant batches keep the split-K tail of o_proj / down_proj (+0.5 %, but the tail's
+# rows then sum their K ranges in another order than the baseline's: not row-exact for those rows)
 EXACT_TAIL_SPLIT = os.environ.get("CRAM_ROW_EXACT_TAIL_SPLIT", "0") == "1"
 
 

@@ -137,7 +137,7 @@ def test_sweep_ie_matches_fp32_truth_at_llama3_8b_shape(setup):
 
 
 def test_unperturbed_rows_are_row_exact(setup):
-    """The opt-in row-exact sweep drops the per-layer un-perturbed variant (sweep.py) because an un-perturbed row
+    """The row-exact sweep (the default since round 6) drops the per-layer un-perturbed variant (sweep.py) because an un-perturbed row
     computes the same bits in the baseline forward as in the whole waves of any variant batch: for the first, a
     middle and the last layer, the un-perturbed variant carried in the batch (with_base=True, the first variant)
     equals the baseline's final hidden state bit for bit, so IE = ori(baseline) - cur is the grid the batch-carried
@@ -150,7 +150,7 @@ def test_unperturbed_rows_are_row_exact(setup):
     sp = eng.spec
     n = ans.numel()
     prev = sweep.ROW_EXACT
-    sweep.ROW_EXACT = True                          # the opt-in mode (CRAM_SWEEP_ROW_EXACT=1)
+    sweep.ROW_EXACT = True                          # the default mode (CRAM_SWEEP_ROW_EXACT=0 turns it off)
     try:
         _row_exact_checks(eng, ids, w16, ans, sweep, CredibilityBias)
     finally:
