@@ -14,6 +14,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of the sweep-only bench (summary kept, traces deleted)
 #   pmc              the attention kernel's PMC passes (tools/pmc_attn.sh) -> pmc_summary.txt + attn_pmc.json
 #   pmcgemm          the dominant GEMM launch's PMC passes (tools/pmc_gemm.sh) -> gemm_pmc_summary.txt + gemm_pmc.json
+#   pmclt            the same passes on hipBLASLt's kernel for the same product -> lt_pmc.json (EXTRA=1: + request sizes)
 #   test:PATTERN     pytest -m gpu -k PATTERN
 #   py:SCRIPT,ARGS   python SCRIPT ARGS (a probe under tools/)
 #   pyt:SEC:SCRIPT,ARGS  the same under a time limit of SEC seconds
@@ -51,6 +52,8 @@ for step in "$@"; do
                python3 tools/pmc_to_json.py $O/pmc $O/attn_pmc.json > /dev/null; cat $O/pmc_summary.txt ;;
     pmcgemm)   OUT=$O/gemm_pmc bash tools/pmc_gemm.sh > $O/gemm_pmc_summary.txt 2>&1
                python3 tools/pmc_to_json.py --gemm $O/gemm_pmc $O/gemm_pmc.json > /dev/null; cat $O/gemm_pmc_summary.txt ;;
+    pmclt)     MODE=lt KREGEX=Cijk OUT=$O/lt_pmc bash tools/pmc_gemm.sh > $O/lt_pmc_summary.txt 2>&1
+               python3 tools/pmc_to_json.py --lt $O/lt_pmc $O/lt_pmc.json > /dev/null; cat $O/lt_pmc_summary.txt ;;
     test:*)    k=${step#test:}; n=$(echo "$k" | tr -c 'a-zA-Z0-9' '_' | cut -c1-60)
                timeout -k 10 900 $PYT -x -v -s -k "$k" > $O/test_$n.txt 2>&1; tail -3 $O/test_$n.txt ;;
     py:*)      a=${step#py:}; n=$(basename "${a%%,*}" .py)$(echo "${a#*,}" | tr -c 'a-zA-Z0-9' '_' | cut -c1-40)
