@@ -392,7 +392,7 @@ class CrAMEngine:
         return h + self.mlp(x2, lw)
 
     def layer_rows(self, hbuf: torch.Tensor, B: int, T: int, l: int, cos, sin, bias=None, enable=None, W: int = 0,
-                   out_rows: Optional[int] = None, delta: Optional[torch.Tensor] = None, prefix=None):
+                   out_rows: Optional[int] = None, delta: Optional[torch.Tensor] = None, prefix=None, join=None):
         """One decoder layer over a ROW buffer: rows [0, B*T) are B sequences of T tokens, rows beyond are
         alignment padding (GEMM M from padded_rows: the 256-row macro tile, then the measured row table; padding rows carry
         garbage and are never read back).  The layer input is hbuf [Mp, D], or hbuf + delta when the previous
@@ -404,7 +404,12 @@ class CrAMEngine:
         prefix=(k0, v0): the B sequences are SUFFIXES that start at position p0 = k0.shape[1] of a common
         prefix whose roped K/V at this layer are k0/v0 [1, p0, Hkv, d] (shared by all B sequences); row t of every
         suffix sits at position p0 + t (the only form: the fused path computes that position, the library path
-        builds the same array).  Attention then runs over p0 + T keys per sequence."""
+        builds the same array).  Attention then runs over p0 + T keys per sequence.
+
+        join=(a_new [M_new, q_size], h_new [M_new, D]): M_new more rows (whole sequences of T rows) enter here, after
+        the attention, with their attention output given (the IE sweep's next perturbed layer, sweep.group_variants):
+        o_proj + MLP run over the B * T rows and those in one launch each; the returned buffers hold B * T + M_new
+        rows (padded as padded_rows picks)."""
         sp, lw = self.spec, self.layers[l]
         M = B * T
         if delta is None:
@@ -457,7 +462,18 @@ class CrAMEngine:
                 ops.rope_split(y[:M], sp.num_heads, sp.num_kv_heads, sp.head_dim, cos, sin, T, k, v, p0, pos=pos)
             y3 = y[:M].view(B, T, -1)
         q = y3[..., :sp.q_size].unflatten(-1, (sp.num_heads, sp.head_dim))
-        if out_rows is None:
+        if out_rows is None and join is not None:
+            a_new, h_new = join
+            Mt = M + a_new.shape[0]
+            Mp = padded_rows(Mt, sp)
+            a = torch.empty((Mp, sp.q_size), dtype=self.dtype, device=self.device)
+            ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale, bias=bias,
+                             enable=enable, W=W, out=a[:M].view(B, T, sp.num_heads, sp.head_dim))
+            a[M:Mt] = a_new
+            hres = torch.empty((Mp, sp.hidden), dtype=self.dtype, device=self.device)
+            hres[:M] = hbuf[:M]
+            hres[M:Mt] = h_new
+        elif out_rows is None:
             a = torch.empty((hbuf.shape[0], sp.q_size), dtype=self.dtype, device=self.device)
             ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale, bias=bias,
                              enable=enable, W=W, out=a[:M].view(B, T, sp.num_heads, sp.head_dim))

@@ -51,6 +51,8 @@ ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "1") == "1"
 # CRAM_ROW_EXACT_TAIL_SPLIT=1: the variant batches keep the split-K tail of o_proj / down_proj (+0.5 %, but the tail's
 # rows then sum their K ranges in another order than the baseline's: not row-exact for those rows)
 EXACT_TAIL_SPLIT = os.environ.get("CRAM_ROW_EXACT_TAIL_SPLIT", "0") == "1"
+# consecutive swept layers whose variant batches share one growing batch (group_variants); 1 = a batch per layer
+SWEEP_GROUP = int(os.environ.get("CRAM_SWEEP_GROUP", "1"))
 
 
 class QuestionCache:
@@ -202,6 +204,95 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     return y.view(Hv, n_ans, sp.hidden)                                 # [Hv, n, D]
 
 
+def _variant_inputs(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tensor, W: int, T: int, b0: int):
+    """The perturbed layer-l inputs of one variant batch over the suffix rows (the last T rows): attention output
+    [Hv * T, q_size] (head h of variant b0 + h from the all-heads-biased call, the rest the baseline's) and the
+    residual input [Hv * T, D]; Hv = H + b0 (b0 = 1: the un-perturbed variant first)."""
+    sp = eng.spec
+    H = sp.num_heads
+    Hv = H + b0
+    enable = torch.ones((1, H), dtype=torch.uint8, device=eng.device)
+    a_bias = eng.attention(qc.q[l][:, -T:], qc.k[l], qc.v[l], bias, enable, W)        # [1, T, Hq, d]
+    a = torch.empty((Hv * T, sp.q_size), dtype=eng.dtype, device=eng.device)
+    x = a.view(Hv, T, H, sp.head_dim)
+    x.copy_(qc.a[l][:, -T:].expand(Hv, T, H, sp.head_dim))
+    heads = torch.arange(H, device=eng.device)
+    x[heads + b0, :, heads] = a_bias[0].permute(1, 0, 2)
+    hin = qc.h_in[l][:, -T:].expand(Hv, T, sp.hidden).reshape(Hv * T, sp.hidden)
+    return a, hin
+
+
+@torch.no_grad()
+def group_variants(eng: CrAMEngine, qc: QuestionCache, ls, bias: torch.Tensor, W: int, n_ans: int, p0: int = 0,
+                   with_base: Optional[bool] = None):
+    """layer_variants for a run of consecutive layers ls (all below the last) in ONE growing batch: the variant batch
+    of ls[0] starts at its layer; at each later layer of ls that layer's batch joins after the attention (its
+    attention output is the perturbed one, the running sequences compute theirs), so o_proj, the MLP and every layer
+    above run over all joined sequences in one launch each -- fewer launches and fuller waves of 256 x 256 tiles than
+    one batch per layer.  Every kernel is row-independent (the 4-wave GEMM's per-element accumulation order does not
+    depend on M or on the row's place; attention per sequence), so each variant's result is the one layer_variants
+    gives (row-exact mode: bit for bit, tests/test_fullsize_ie_gpu.py).  Returns {l: [Hv, n, D]}."""
+    sp = eng.spec
+    L, H = sp.num_layers, sp.num_heads
+    ls = list(ls)
+    assert ls and all(b == a + 1 for a, b in zip(ls, ls[1:])) and ls[-1] < L - 1, ls
+    if with_base is None:
+        with_base = not qc.exact
+    b0 = 1 if with_base else 0
+    Hv = H + b0
+    T_full = qc.h_in[ls[0]].shape[1]
+    p0 = max(0, min(int(p0), T_full - n_ans))
+    T = T_full - p0
+    cos, sin = eng.rope_tables(T_full)
+    h = m = None
+    nseq = 0
+    with _modes(eng, qc.exact, qc.exact and not EXACT_TAIL_SPLIT):
+        for l2 in range(ls[0], L):
+            pre = None if p0 == 0 else (qc.k[l2][:, :p0], qc.v[l2][:, :p0])
+            join = _variant_inputs(eng, qc, l2, bias, W, T, b0) if l2 in ls else None
+            if nseq == 0:                                               # the first batch: layer_variants' start
+                lw = eng.layers[l2]
+                M = Hv * T
+                Mp = padded_rows(M, sp)
+                abuf = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=eng.device)
+                hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
+                abuf[:M] = join[0]
+                hin[:M] = join[1]
+                h, x2 = eng.o_proj_norm(abuf, lw, hin)
+                h, m = eng.mlp_residual(x2, lw, h)
+            else:
+                h, m = eng.layer_rows(h, nseq, T, l2, cos, sin, out_rows=n_ans if l2 == L - 1 else None, delta=m,
+                                      prefix=pre, join=join)
+            if join is not None:
+                nseq += Hv
+    rows = nseq * n_ans
+    if m is None:
+        y = ops.rmsnorm(h[:rows], eng.norm, sp.eps)
+    else:
+        _, y = ops.rmsnorm(m[:rows], eng.norm, sp.eps, residual=h[:rows])
+    y = y.view(len(ls), Hv, n_ans, sp.hidden)
+    return {l: y[i] for i, l in enumerate(ls)}
+
+
+def sweep_groups(layers, num_layers: int, group: int):
+    """Runs of at most `group` consecutive layers below the last (group_variants), the last layer alone."""
+    out, run = [], []
+    for l in sorted(layers):
+        if l == num_layers - 1 or group <= 1:
+            if run:
+                out.append(run)
+                run = []
+            out.append([l])
+            continue
+        if run and (l != run[-1] + 1 or len(run) == group):
+            out.append(run)
+            run = []
+        run.append(l)
+    if run:
+        out.append(run)
+    return out
+
+
 @torch.no_grad()
 def ie_question(eng: CrAMEngine, ids: torch.Tensor, weight16: torch.Tensor, answer_ids: torch.Tensor,
                 layers=None, round_logits: bool = False, skip_prefix: bool = True) -> torch.Tensor:
@@ -238,10 +329,15 @@ def _ie_question(eng, ids, weight16, answer_ids, layers, round_logits, skip_pref
     Hv = H if qc.exact else H + 1
     ans_rep = ans.repeat(Hv)
     ori = _answer_sums(eng.answer_logits(hf, ans, round_logits).view(1, n))[0] if qc.exact else None
-    for i, l in enumerate(layers):
-        hv = layer_variants(eng, qc, l, cb.bias, cb.W, n, p0=p0)       # [Hv, n, D]
-        sums = _answer_sums(eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_logits).view(Hv, n))
-        out[i] = ori - sums if qc.exact else sums[0] - sums[1:]        # ori - cur
+    pos = {l: i for i, l in enumerate(layers)}
+    for grp in sweep_groups(layers, sp.num_layers, SWEEP_GROUP):
+        if len(grp) == 1:
+            hvs = {grp[0]: layer_variants(eng, qc, grp[0], cb.bias, cb.W, n, p0=p0)}      # [Hv, n, D]
+        else:
+            hvs = group_variants(eng, qc, grp, cb.bias, cb.W, n, p0=p0)
+        for l, hv in hvs.items():
+            sums = _answer_sums(eng.answer_logits(hv.reshape(-1, sp.hidden), ans_rep, round_logits).view(Hv, n))
+            out[pos[l]] = ori - sums if qc.exact else sums[0] - sums[1:]   # ori - cur
     return out
 
 

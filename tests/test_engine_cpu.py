@@ -471,6 +471,26 @@ def test_sweep_prefix_skip_is_exact(tiny, nq):
 
 
 
+@pytest.mark.parametrize("kind", ["llama3", "qwen2"])
+def test_sweep_grouped_batches_equal_per_layer_batches(tiny, nq, kind, monkeypatch):
+    """group_variants (consecutive swept layers in one growing batch, each layer's batch joining after its attention)
+    computes the variants layer_variants does: the same IE grid as one batch per layer, with and without the prefix
+    skip, for every grouping (on the GPU's row-independent kernels bit for bit, tests/test_fullsize_ie_gpu.py)."""
+    path, tok, model = tiny[kind]
+    eng = CrAMEngine.from_hf(model)
+    ids, w = _question(tok, path, nq[1])
+    ans = tok([nq[1]["wrong_answer"]], return_tensors="pt")["input_ids"][0, 1:]
+    assert sweep.sweep_groups(range(eng.spec.num_layers), eng.spec.num_layers, 2)[-1] == [eng.spec.num_layers - 1]
+    with cpu_ops.patched_ops():
+        for skip in (True, False):
+            monkeypatch.setattr(sweep, "SWEEP_GROUP", 1)
+            a = sweep.ie_question(eng, ids[0], w[0], ans, skip_prefix=skip)
+            for g in (2, 3):
+                monkeypatch.setattr(sweep, "SWEEP_GROUP", g)
+                b = sweep.ie_question(eng, ids[0], w[0], ans, skip_prefix=skip)
+                assert (a - b).abs().max() <= 1e-3 * max(1.0, float(a.abs().max())), (skip, g, (a - b).abs().max())
+
+
 def test_padded_rows_table():
     """GEMM row padding: a multiple of 256, never fewer rows, at most +2048 with the Llama-3-8B table; other
     shapes (and no spec) keep plain 256-row rounding."""

@@ -157,6 +157,26 @@ def test_unperturbed_rows_are_row_exact(setup):
         sweep.ROW_EXACT = prev
 
 
+def test_grouped_batches_are_bit_identical(setup):
+    """sweep.group_variants at the Llama-3-8B shape: consecutive swept layers in one growing batch (each joining
+    after its own attention) give the IE grid one batch per layer gives, bit for bit in the row-exact mode -- the
+    4-wave GEMM rounds a row the same whatever M and the row's place, attention and RMSNorm are per sequence / row."""
+    from cram_amd import sweep
+    eng, ids, w16, ans = setup
+    layers = [0, 1, 2, 3, 4, 5, 28, 29, 30, 31]
+    prev = sweep.SWEEP_GROUP
+    try:
+        sweep.SWEEP_GROUP = 1
+        a = sweep.ie_question(eng, ids, w16, ans, layers=layers)
+        for g in (3, 4):
+            sweep.SWEEP_GROUP = g
+            b = sweep.ie_question(eng, ids, w16, ans, layers=layers)
+            assert sweep.row_exact(eng)
+            assert torch.equal(a, b), (g, (a - b).abs().max().item())
+    finally:
+        sweep.SWEEP_GROUP = prev
+
+
 def _row_exact_checks(eng, ids, w16, ans, sweep, CredibilityBias):
     sp = eng.spec
     n = ans.numel()
