@@ -303,7 +303,8 @@ def main():
             # algorithmic (SURVEY §8(d) with the prefix skip: 32 variants, answer-row q in the last layer) and what
             # the sweep executes (+ the un-perturbed variant of the default mode, the GEMMs' pad rows)
             flops += sweep.sweep_flops(spec, T, n_ans, p0, layers)
-            flops_ex += sweep.sweep_flops_executed(spec, T, n_ans, p0, layers, base_variant=base_variant)
+            flops_ex += sweep.sweep_flops_executed(spec, T, n_ans, p0, layers, base_variant=base_variant,
+                                                   group=sweep.SWEEP_GROUP)
         ksum = ops.TIMER.summary()
         kt = ksum.get("cram_prefill", None)
         # the projections: cram_gemm (gemm_w4_kernel, every epilogue), its split-K tail, and F.linear calls left

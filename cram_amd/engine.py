@@ -108,16 +108,19 @@ PREFIX_SHARE_MIN_ROWS = 16
 SHARED_DECODE_READ = os.environ.get("CRAM_SHARED_DECODE_READ", "1") != "0"
 
 
-def padded_rows(M: int, spec: Optional["ModelSpec"] = None) -> int:
+def padded_rows(M: int, spec: Optional["ModelSpec"] = None, no_tail: bool = False) -> int:
     """GEMM row count for M rows: rounded up to the 256-row macro tile and, for the Llama-3-8B projection shapes, to
     the row count within +2048 that minimises the measured per-layer GEMM time plus the per-row non-GEMM work
     (data/gemm_rows.json, the engine's own fused GEMMs with the residual tail split: ~311-314 ns per row at most
-    row counts, 307-309 at multiples of 4096; round 3's hipBLASLt table had 290 vs 305-315)."""
+    row counts, 307-309 at multiples of 4096; round 3's hipBLASLt table had 290 vs 305-315).  no_tail: the table of
+    the same GEMMs without the split-K tail (the IE sweep's row-exact batches, 16k-131k rows: their grouped batches
+    reach ~120k rows), where a row count whose N = 4096 tiles end in a sparse wave costs that whole wave."""
     Mp = -(-M // ROW_ALIGN) * ROW_ALIGN
-    tab = _row_table(spec)
+    tab = _row_table(spec, no_tail)
     if tab is None or Mp not in tab:
         return Mp
-    cands = [m for m in range(Mp, Mp + 2049, ROW_ALIGN) if m in tab]
+    # within +2048 rows, or +1/16 of M for the grouped sweep batches (~60-120k rows)
+    cands = [m for m in range(Mp, Mp + max(2048, Mp // 16) + 1, ROW_ALIGN) if m in tab]
     return min(cands, key=lambda m: (tab[m] + ROW_COST_MS * m, m))
 
 
@@ -127,10 +130,10 @@ ROW_COST_MS = 19e-6
 _ROW_TABLES = {}
 
 
-def _row_table(spec) -> Optional[dict]:
+def _row_table(spec, no_tail: bool = False) -> Optional[dict]:
     if spec is None or os.environ.get("CRAM_ROW_TABLE", "1") == "0":    # A/B switch: plain 256-row rounding
         return None
-    key = (spec.hidden, spec.intermediate, spec.q_size + 2 * spec.kv_size)
+    key = (spec.hidden, spec.intermediate, spec.q_size + 2 * spec.kv_size, no_tail)
     if key not in _ROW_TABLES:
         import json
         fn = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "gemm_rows.json")
@@ -139,8 +142,9 @@ def _row_table(spec) -> Optional[dict]:
             with open(fn) as f:
                 d = json.load(f)
             shp = d["shape"]
-            if key == (shp["hidden"], shp["intermediate"], shp["qkv"]):
-                tab = {int(m): float(t) for m, t in d["layer_gemm_ms"].items()}
+            name = "layer_gemm_ms_no_tail" if no_tail else "layer_gemm_ms"
+            if key[:3] == (shp["hidden"], shp["intermediate"], shp["qkv"]) and name in d:
+                tab = {int(m): float(t) for m, t in d[name].items()}
         except (OSError, ValueError, KeyError):
             tab = None
         _ROW_TABLES[key] = tab
@@ -465,7 +469,7 @@ class CrAMEngine:
         if out_rows is None and join is not None:
             a_new, h_new = join
             Mt = M + a_new.shape[0]
-            Mp = padded_rows(Mt, sp)
+            Mp = padded_rows(Mt, sp, no_tail=self.no_tail_split)
             a = torch.empty((Mp, sp.q_size), dtype=self.dtype, device=self.device)
             ops.attn_prefill(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2), scale=self.scale, bias=bias,
                              enable=enable, W=W, out=a[:M].view(B, T, sp.num_heads, sp.head_dim))

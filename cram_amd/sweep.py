@@ -51,8 +51,11 @@ ROW_EXACT = os.environ.get("CRAM_SWEEP_ROW_EXACT", "1") == "1"
 # CRAM_ROW_EXACT_TAIL_SPLIT=1: the variant batches keep the split-K tail of o_proj / down_proj (+0.5 %, but the tail's
 # rows then sum their K ranges in another order than the baseline's: not row-exact for those rows)
 EXACT_TAIL_SPLIT = os.environ.get("CRAM_ROW_EXACT_TAIL_SPLIT", "0") == "1"
-# consecutive swept layers whose variant batches share one growing batch (group_variants); 1 = a batch per layer
-SWEEP_GROUP = int(os.environ.get("CRAM_SWEEP_GROUP", "1"))
+# consecutive swept layers whose variant batches share one growing batch (group_variants; bit-identical IE in the
+# row-exact mode): groups of 4 ran 222.0 heads/s against 218.4 for a batch per layer (2: 221.0, 8: 220.6, whose
+# ~230k-row buffers cost the allocator more than the fuller waves return), same box, profiles/r06/group/;
+# CRAM_SWEEP_GROUP=1 runs a batch per layer (A/B)
+SWEEP_GROUP = int(os.environ.get("CRAM_SWEEP_GROUP", "4"))
 
 
 class QuestionCache:
@@ -175,7 +178,8 @@ def layer_variants(eng: CrAMEngine, qc: QuestionCache, l: int, bias: torch.Tenso
     a_bias = eng.attention(q, k, v, bias, enable, W)                   # [1, rows, Hq, d] every head biased
     a_base = qc.a[l][:, -rows:]
     M = Hv * rows
-    Mp = M if last else padded_rows(M, sp)                              # GEMM rows: macro tile / measured table
+    no_tail = qc.exact and not EXACT_TAIL_SPLIT
+    Mp = M if last else padded_rows(M, sp, no_tail)                     # GEMM rows: macro tile / measured table
     abuf = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=eng.device)
     x = abuf[:M].view(Hv, rows, H, sp.head_dim)
     x.copy_(a_base.expand(Hv, rows, H, sp.head_dim))                    # [Hv, rows, Hq, d]
@@ -253,7 +257,7 @@ def group_variants(eng: CrAMEngine, qc: QuestionCache, ls, bias: torch.Tensor, W
             if nseq == 0:                                               # the first batch: layer_variants' start
                 lw = eng.layers[l2]
                 M = Hv * T
-                Mp = padded_rows(M, sp)
+                Mp = padded_rows(M, sp, eng.no_tail_split)
                 abuf = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=eng.device)
                 hin = torch.empty((Mp, sp.hidden), dtype=eng.dtype, device=eng.device)
                 abuf[:M] = join[0]
@@ -380,10 +384,12 @@ def sweep_flops(spec, T: int, n_ans: int, p0: int = 0, layers=None) -> float:
     return f
 
 
-def sweep_flops_executed(spec, T: int, n_ans: int, p0: int = 0, layers=None, base_variant: bool = True) -> float:
+def sweep_flops_executed(spec, T: int, n_ans: int, p0: int = 0, layers=None, base_variant: bool = True,
+                         group: int = 1) -> float:
     """The GEMM + attention flops ie_question EXECUTES: sweep_flops plus the un-perturbed variant each batch carries
-    (base_variant: the default, not row-exact mode), the pad rows of the suffix layers' GEMMs (engine.padded_rows:
-    the 256-row macro tile, then the measured row table) and the baseline forward's last-layer q over every row."""
+    (base_variant: the mode without row-exactness), the pad rows of the suffix layers' GEMMs (engine.padded_rows: the
+    256-row macro tile, then the measured row table) with the batches grouped as sweep_groups(.., group) groups them,
+    and the baseline forward's last-layer q over every row."""
     from .engine import padded_rows
     L, H = spec.num_layers, spec.num_heads
     Hv = H + 1 if base_variant else H
@@ -391,16 +397,23 @@ def sweep_flops_executed(spec, T: int, n_ans: int, p0: int = 0, layers=None, bas
     p0 = max(0, min(p0, T - n_ans))
     Ts = T - p0
     lay = fq + fkv + frest
-    Mp = padded_rows(Hv * Ts, spec)                                     # GEMM rows of a suffix batch
     f = (L - 1) * (lay * T + attn(T, T)) + (fq + fkv) * T + frest * n_ans + attn(n_ans, T)
-    for l in (range(L) if layers is None else layers):
-        last = l == L - 1
-        rows = n_ans if last else Ts
-        f += attn(rows, T)
-        f += frest * (Hv * n_ans if last else Mp)                       # o_proj + MLP of layer l over the batch
-        for l2 in range(l + 1, L):
-            if l2 == L - 1:
-                f += fkv * Mp + (fq + frest) * Hv * n_ans + Hv * attn(n_ans, T)
-            else:
-                f += lay * Mp + Hv * attn(Ts, T)
+    for grp in sweep_groups(range(L) if layers is None else layers, L, group):
+        if grp == [L - 1]:                                              # the last layer: answer rows only
+            f += attn(n_ans, T) + frest * Hv * n_ans
+            continue
+        nseq = 0
+        m_prev = 0                                                      # padded rows of the running batch
+        for l2 in range(grp[0], L):
+            joins = l2 in grp
+            if joins:
+                f += attn(Ts, T)                                        # the joining layer's biased attention
+            if nseq:                                                    # the running sequences' own layer l2
+                if l2 == L - 1:
+                    f += fkv * m_prev + (fq + frest) * nseq * n_ans + nseq * attn(n_ans, T)
+                    continue
+                f += (fq + fkv) * m_prev + nseq * attn(Ts, T)
+            nseq += Hv if joins else 0
+            m_prev = padded_rows(nseq * Ts, spec, no_tail=not base_variant)
+            f += frest * m_prev                                         # o_proj + MLP over every row of the batch
     return f
