@@ -41,8 +41,9 @@ def record(family: str, ours: float, ref: float, **extra) -> None:
 class Aggregate:
     """Samples of one test: add() records and applies the per-sample guard, check() the aggregate bar."""
 
-    def __init__(self, cpu: bool = False):
+    def __init__(self, cpu: bool = False, label: str = ""):
         self.cpu = cpu
+        self.label = label          # a subset reported beside the test's own aggregate (log_aggregates)
         self.sums = {}
 
     def add(self, family: str, ours: float, ref: float, **extra) -> None:
@@ -69,7 +70,7 @@ class Aggregate:
     def log_aggregates(self) -> None:
         """Record the aggregates without a bar (a subset reported beside a test's own aggregate)."""
         for family, (o, r, n) in self.sums.items():
-            record(family + "_aggregate", o, r, samples=n, informative_samples=n)
+            record(family + "_aggregate", o, r, samples=n, informative_samples=n, subset=self.label)
 
     def check(self) -> None:
         bars = AGG_F_CPU if self.cpu else AGG_F

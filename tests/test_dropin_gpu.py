@@ -53,7 +53,8 @@ def _gold_files(kind):
 def _first3(agg_all, kind, ie_err, ref_err, idx):
     """The original three Qwen2 questions (idx 0-2) as their own logged aggregate."""
     if kind == "qwen2" and idx < 3:
-        agg_all.setdefault("first3", parity.Aggregate()).ie_errors(ie_err, ref_err, subset="qwen2 idx 0-2", idx=idx)
+        agg_all.setdefault("first3", parity.Aggregate(label="qwen2 idx 0-2")).ie_errors(ie_err, ref_err,
+                                                                                       subset="qwen2 idx 0-2", idx=idx)
 
 
 @pytest.fixture(scope="module")
