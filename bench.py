@@ -197,7 +197,11 @@ def main():
     ap.add_argument("--dist-backend", default=None, help="nccl (RCCL, default on GPU) or gloo (rehearsal)")
     ap.add_argument("--model", default=None, choices=["llama3-8b", "qwen2-7b", "llama2-13b"],
                     help="override the config's model: llama2-13b = the reference's default model (fp16, MHA)")
+    ap.add_argument("--expandable-segments", action="store_true",
+                    help="PYTORCH_HIP_ALLOC_CONF=expandable_segments:True (A/B of the caching allocator's segments)")
     args = ap.parse_args()
+    if args.expandable_segments:
+        os.environ["PYTORCH_HIP_ALLOC_CONF"] = "expandable_segments:True"      # before torch initialises HIP
 
     import torch
     from cram_amd import dist as cdist
