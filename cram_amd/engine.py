@@ -932,6 +932,11 @@ class DecodeSession:
             h[total:].zero_()
         bias = self.cb.bias[b0:b1]
         last = cu[1:].long() - 1                     # each sequence's last row: the only one the logits need
+        # the attention output of every layer: the kernels write rows :total, so the pad rows o_proj reads are zeroed
+        # once per chunk, not once per layer
+        a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
+        if Mp > total:
+            a[total:].zero_()
         m = None                                     # pending MLP output: layer output = h + m (add fused below)
         for l, lw in enumerate(eng.layers):
             if m is None:
@@ -964,9 +969,6 @@ class DecodeSession:
                 break
             k = yr[:, sp.q_size:sp.q_size + sp.kv_size].view(total, sp.num_kv_heads, sp.head_dim)
             v = yr[:, sp.q_size + sp.kv_size:].view(total, sp.num_kv_heads, sp.head_dim)
-            a = torch.empty((Mp, sp.q_size), dtype=eng.dtype, device=dev)
-            if Mp > total:
-                a[total:].zero_()
             if p:                                    # keys: the cached prefix, then the suffix's own rows
                 ops.attn_prefill_varlen_cached(q, kc[b0:b1], vc[b0:b1], cu, max(lens), p, scale=eng.scale, bias=bias,
                                                enable=self.cb.enable[l, b0:b1], W=self.cb.W,
