@@ -587,11 +587,12 @@ class CrAMEngine:
 # profiles/r03/decode_gemm_probe_*.jsonl): only the long-K down projection wins (Llama-3 N 4096 x K 14336: 55.9 vs
 # 62.9 us at 8 ranges = 128 workgroups); at K <= N (q/k/v, o_proj, gate/up, lm_head) the fp32 partial slabs and
 # their combine cost more than the library loses, so those stay on F.linear.  CRAM_DECODE_GEMM=0 turns it off (A/B).
-DECODE_GEMM_MAX_ROWS = int(os.environ.get("CRAM_DECODE_GEMM_MAX_ROWS", "512"))   # A/B override
+DECODE_GEMM_MAX_ROWS = int(os.environ.get("CRAM_DECODE_GEMM_MAX_ROWS", "1024"))  # A/B override
 DECODE_GEMM_TARGET_WGS = 128
 DECODE_GEMM_MIN_K_OVER_N = 2
 DECODE_QKV_SPLIT_MAX_ROWS = 192
 DECODE_MLP_W4_MIN_ROWS = int(os.environ.get("CRAM_DECODE_MLP_W4_MIN_ROWS", "384"))
+DECODE_SPLIT_ROW_TILES = os.environ.get("CRAM_DECODE_SPLIT_ROW_TILES", "1") == "1"   # A/B (decode_splits)
 
 
 def decode_splits(N: int, K: int, rows: int) -> int:
@@ -608,6 +609,14 @@ def decode_splits(N: int, K: int, rows: int) -> int:
     # at <= 192 rows more ranges pay: Llama-3 down at 129 rows 41.9 us at 14 ranges (224 workgroups) vs 48.0 at 8
     # (profiles/r04/dec129/)
     target = DECODE_GEMM_TARGET_WGS if rows > DECODE_QKV_SPLIT_MAX_ROWS else 224
+    if rows > 512 and DECODE_SPLIT_ROW_TILES:
+        # beyond 512 rows the row tiles multiply the grid (and the fp32 partial slabs the combine reads): count them
+        # and aim at one workgroup per CU -- down_proj at 1,000 rows over 4 K ranges on the 4-wave kernel (256
+        # workgroups) instead of hipBLASLt's 128 x 128 tiles: config 2 steps 35.0 -> 34.3 ms, config 4 (Qwen2-7B)
+        # 27.3 -> 25.7 ms, same box (profiles/r06/s2/decode_down_split_ab.txt); the column-tile rule alone gave 8
+        # ranges (512 workgroups, twice the partial bytes) and lost there (34.9 ms)
+        tiles *= -(-rows // 256)
+        target = 256
     for s in range(1, K // 256 + 1):
         if K % (64 * s):
             continue

@@ -152,14 +152,14 @@ def test_config2_step_at_500_rows(l3w, monkeypatch, n):
     """Config 2's timed batch -- round 6: NQ-1000 in ONE batch of 1000 rows (bench --decode-batch 1024, KV cache in
     0.68 of HBM; 81.8 vs 79.5 questions/s for two batches of 500, profiles/r06/decode_b*.json), and the 500-row batch
     of rounds 3-5: gate/up + SiLU-mul and lm_head on gemm_w4_kernel inside the captured step graph, down_proj over 8 K
-    ranges up to DECODE_GEMM_MAX_ROWS (the library beyond), q/k/v / o_proj on the library; the shared prompt opening
-    read from cache row 0 by the decode attention."""
+    ranges at 500 rows and 4 at 1000 (the row tiles counted beyond 512 rows: one workgroup per CU), q/k/v / o_proj on
+    the library; the shared prompt opening read from cache row 0 by the decode attention."""
     from cram_amd import engine as E
     eng, tok, heads = l3w
     prompts, ws = _encode(tok, n)
     new = 12
     rt = _routing(eng, prompts, ws, heads, new)
-    assert (rt["mlp_w4"] and rt["lm_w4"] and rt["down"] == (8 if n <= E.DECODE_GEMM_MAX_ROWS else 0)
+    assert (rt["mlp_w4"] and rt["lm_w4"] and rt["down"] == {500: 8, 1000: 4}[n] and n <= E.DECODE_GEMM_MAX_ROWS
             and rt["qkv"] == 0 and rt["o"] == 0 and rt["gu"] == 0 and not rt["small"]), rt
     got = eng.generate(prompts, ws, heads, max_new_tokens=new, use_graph=True, stop_on_eos=False)
     assert eng.generate(prompts[:3], ws[:3], heads, max_new_tokens=new, use_graph=False, stop_on_eos=False) is not None

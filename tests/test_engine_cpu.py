@@ -502,3 +502,14 @@ def test_padded_rows_table():
         assert padded_rows(M) == -(-M // 256) * 256
         assert padded_rows(M, ModelSpec.qwen2_7b()) == padded_rows(M)
     assert padded_rows(32400, sp) == 32768        # measured: 32768 rows (8 x 4096) run cheaper than 32512
+
+
+def test_decode_split_plan():
+    """K ranges of the decode step's long-K down_proj (engine.decode_splits): column tiles toward 128 workgroups up to
+    512 rows (8 ranges for Llama-3 at 256 / 500 rows, 14 at config 5's 129), the row tiles counted beyond 512 rows
+    toward one workgroup per CU (4 ranges at 1,000 rows for Llama-3 and Qwen2-7B), the library past 1,024 rows; the
+    short-K projections stay on the library."""
+    ds = engine_mod.decode_splits
+    assert [ds(4096, 14336, r) for r in (129, 256, 500, 512, 1000, 1024, 1025)] == [14, 8, 8, 8, 4, 4, 0]
+    assert ds(3584, 18944, 1000) == 4 and ds(3584, 18944, 500) == 8
+    assert ds(6144, 4096, 1000) == 0 and ds(4096, 4096, 1000) == 0 and ds(28672, 4096, 1000) == 0
