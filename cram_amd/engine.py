@@ -738,10 +738,15 @@ class DecodeSession:
         # (N 37,888, K 3,584: 167.8 vs 153.1; config 4 steps 13.9 -> 14.5 ms), profiles/r04/dec129/, decq/; the
         # interleaved weight is built here, outside the step graph
         # CRAM_DECODE_MLP_W4=1 / 0 forces it on / off at any shape the kernel takes (A/B of other shapes)
+        # "auto": when the kernel's 256 x 256 tiles fill at least 3/4 of the CU waves they take -- Llama-3 at 512 and
+        # 1,000 rows (224 / 448 tiles: 0.875), Qwen2-7B at 1,000 rows (592 tiles: 0.77; steps 25.5 -> 23.1 ms against
+        # hipBLASLt + silu_mul, profiles/r06/s2/decode_qwen2_gateup_w4_ab.txt) but not at 512 (296 tiles: 0.58, the
+        # column tail below)
         w4_env = os.environ.get("CRAM_DECODE_MLP_W4", "auto")
+        gu_tiles = -(-self.B // 256) * (2 * sp.intermediate // 256)
+        gu_fill = gu_tiles / (-(-gu_tiles // eng.num_cus) * eng.num_cus) if eng.device.type == "cuda" else 0.0
         self.mlp_w4 = (not self.splits_gemm["gu"] and self.B >= DECODE_MLP_W4_MIN_ROWS and eng.device.type == "cuda"
-                       and ((2 * sp.intermediate, sp.hidden) == (28672, 4096) if w4_env == "auto"   # measured shape
-                            else w4_env == "1")
+                       and (gu_fill >= 0.75 if w4_env == "auto" else w4_env == "1")
                        and eng._fused_mlp_ok(torch.empty((self.B, sp.hidden), dtype=eng.dtype, device="meta"))
                        and os.environ.get("CRAM_DECODE_GEMM", "1") != "0")
         # gate/up where the 4-wave kernel's 256 x 256 tiles spill just past one wave of the CUs (Qwen2-7B at 512 rows:
